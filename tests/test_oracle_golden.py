@@ -1,0 +1,138 @@
+"""Pin the CPU oracle (oracle/model.py) to the golden fixtures made from the reference itself."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model as om
+from oracle.params import tensor_summary
+from tests._util import fixture, grad_norm_stats, plan, rel_err
+
+# step-level gradient bar (see tests/_util.py:grad_norm_stats for why it is norm-based)
+# D-step: GP double backward; G-step: ~100 sequential BN layers at B=4 (BN1d over 4 samples
+# amplifies rounding where a feature is nearly constant across the batch)
+D_BAR = dict(median=2e-4, p99=2e-3, max=2e-2, vec=1e-3)
+G_BAR = dict(median=2e-4, p99=5e-3, max=1e-1, vec=1e-3)
+
+
+def check_grads(rows, want, bar):
+    med, p99, mx, vec = grad_norm_stats(rows, want)
+    assert med < bar["median"] and p99 < bar["p99"], (med, p99, mx, vec)
+    assert mx < bar["max"] and vec < bar["vec"], (med, p99, mx, vec)
+
+torch.set_num_threads(8)
+
+
+@pytest.fixture(scope="module")
+def P():
+    return plan()
+
+
+def _g(P):
+    return om.params_from_plan(P["g_params"], P["g_seed"])
+
+
+def _d(P):
+    return om.params_from_plan(P["d_params"], P["d_seed"])
+
+
+def test_g_forward_b4(P):
+    fx = fixture("g_fwd_b4.npz")
+    GP = _g(P)
+    draw = om.Draw(101)
+    with torch.no_grad():
+        out = om.generator(GP, torch.from_numpy(fx["z"]), draw.randn)
+    assert rel_err(out, fx["out"]) < 1e-4
+    # the 253 in-forward noise draws happen in the reference's order and shapes
+    assert [list(s) for _, s in draw.log] == P["g_noise_shapes_b4"]
+    # every parameter the reference owns is used (except frozen smooth kernels)
+    names = {n for n, k, _ in P["g_params"] if k != "smooth"}
+    assert GP.used == names
+    # BN running statistics after one train-mode forward
+    buf = []
+    for name in P["g_buffers"]:
+        mod, leaf = name.rsplit(".", 1)
+        rm, rv = GP.buffers[mod]
+        t = {"running_mean": rm, "running_var": rv, "num_batches_tracked": torch.tensor(1.0)}[leaf]
+        buf.append([float(t.double().sum()), float(t.double().norm())])
+    assert rel_err(np.asarray(buf), fx["buffers"]) < 1e-4
+
+
+@pytest.mark.parametrize("B", [4, 8])
+def test_d_forward(P, B):
+    fx = fixture("d_fwd.npz")
+    DP = _d(P)
+    x = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(200 + B))
+    with torch.no_grad():
+        out = om.discriminator(DP, x)
+    assert rel_err(out, fx[f"out_b{B}"]) < 1e-5
+    names = {n for n, k, _ in P["d_params"] if k != "smooth"}
+    assert DP.used == names
+
+
+@pytest.mark.parametrize("B,img_seed,rng_seed", [(4, 300, 301), (8, 310, 311)])
+def test_d_step(P, B, img_seed, rng_seed):
+    fx = fixture(f"d_step_b{B}.npz")
+    GP, DP = _g(P), _d(P)
+    tr = om.WGANGP(GP, DP)
+    images = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed))
+    before = {k: v.detach().clone() for k, v in DP.t.items()}
+    draw = om.Draw(rng_seed)
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, B, draw)]
+    assert rel_err(losses, fx["losses"]) < 1e-4
+    order = [n for n, k, _ in P["d_params"]]
+    rows, deltas = [], []
+    for n in order:
+        if n in DP.t and DP.t[n].grad is not None:
+            rows.append(tensor_summary(DP.t[n].grad))
+            deltas.append(tensor_summary((DP.t[n].detach() - before[n]) / 4e-4))
+        else:
+            rows.append([np.nan] * 11)
+            deltas.append([0.0] * 11)  # untouched by AdamW (grad None)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx["has_grad"]).all()
+    check_grads(rows, fx["grads"], D_BAR)
+    # AdamW step 1 is ~lr*sign(g): compare the delta table loosely (signs of ~0 grads may flip)
+    dl = np.asarray(deltas)
+    ok = ~np.isnan(fx["deltas"][:, 1])
+    assert rel_err(dl[ok, 1], fx["deltas"][ok, 1]) < 1e-3
+
+
+def test_g_step(P):
+    fx = fixture("g_step_b4.npz")
+    GP, DP = _g(P), _d(P)
+    tr = om.WGANGP(GP, DP)
+    draw = om.Draw(401)
+    gen, g_loss = tr.generator_trainstep(4, draw)
+    assert rel_err([float(g_loss)], fx["g_loss"]) < 1e-4
+    assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-4
+    order = [n for n, k, _ in P["g_params"]]
+    rows = []
+    for n in order:
+        t = GP.t.get(n)
+        rows.append(tensor_summary(t.grad) if t is not None and t.grad is not None else [np.nan] * 11)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx["has_grad"]).all()
+    check_grads(rows, fx["grads"], G_BAR)
+
+
+def test_gp_conditioning(P):
+    """Documents WHY step gradients are compared by norms: a 1e-6 relative perturbation of the
+    fake batch moves GP gradients of some D tensors by >1e-5 relative (measured ~1e-4)."""
+    DP = _d(P)
+    B = 8
+    xr = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(310))
+    xf = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(999)) * 0.5
+
+    def gp(xfake):
+        for t in DP.t.values():
+            t.grad = None
+        eps = torch.rand(B, generator=torch.Generator().manual_seed(5)).view(B, 1, 1, 1)
+        xi = ((1 - eps) * xr + eps * xfake).detach().requires_grad_()
+        g = torch.autograd.grad(om.discriminator(DP, xi).sum(), xi, create_graph=True)[0]
+        (10 * ((g.pow(2).view(B, -1).sum(1).sqrt() - 1).pow(2).mean())).backward()
+        return {k: v.grad.clone() for k, v in DP.t.items() if v.grad is not None}
+
+    a = gp(xf)
+    b = gp(xf * (1 + 1e-6 * torch.randn(xf.shape, generator=torch.Generator().manual_seed(7))))
+    worst = max(float((a[k] - b[k]).norm() / a[k].norm()) for k in a)
+    assert worst > 1e-5
