@@ -1,0 +1,107 @@
+"""ctypes binding of libganamd.so (the C ABI declared in include/ganamd.h).
+
+The product path has no fallback: if the shared library is missing or was built for another
+target, importing this module raises.  Every wrapper checks dtype/device/contiguity before
+handing raw pointers to the ABI and launches on torch's current HIP stream, so the calls are
+captured by ``torch.cuda.graph`` like any other kernel.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_HERE, "libganamd.so")
+
+c_int = ctypes.c_int
+c_long = ctypes.c_long
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+vp = ctypes.c_void_p
+
+PAD_ZERO, PAD_REPLICATE = 0, 1
+CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("B", "Cin", "H", "W", "Cout", "OH", "OW", "KH", "KW", "stride", "pad", "pad_mode", "transposed")]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "ganamd_version": (ctypes.c_char_p, []),
+    "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
+    "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp]),
+    "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),
+    "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp]),
+    "ganamd_rowreduce_workspace": (c_size_t, [c_int, c_long]),
+    "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, vp]),
+    "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "ganamd_prelu_fwd": (c_int, [vp, vp, c_int, c_long, vp, vp]),
+    "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, vp, vp]),
+    "ganamd_prelu_bwd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_long, vp, vp, vp, vp, vp]),
+    "ganamd_resample2d": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int, vp]),
+    "ganamd_plane_dot": (c_int, [vp, vp, c_long, c_long, c_float, vp, vp]),
+    "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, vp, vp]),
+    "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),
+    "ganamd_adamw": (c_int, [vp, vp, vp, vp, c_long, vp, c_float, c_float, c_float, c_float, c_float, vp]),
+}
+
+EXPORTS = tuple(_SIGS)
+
+
+def _load():
+    if not os.path.exists(SO_PATH):
+        raise ImportError(f"{SO_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(SO_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+class GanAmdError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise GanAmdError(f"{what} failed with code {rc}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    """Raw device pointer of a contiguous fp32 CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+        raise GanAmdError(f"expected contiguous float32 HIP tensor, got {t.dtype} {t.device} "
+                          f"contiguous={t.is_contiguous()} shape={tuple(t.shape)}")
+    return t.data_ptr()
+
+
+def iptr(t):
+    if t is None:
+        return None
+    if not (t.is_cuda and t.dtype == torch.int32 and t.is_contiguous()):
+        raise GanAmdError("expected contiguous int32 HIP tensor")
+    return t.data_ptr()
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Caller-provided scratch from torch's caching allocator (graph-capture safe)."""
+    return torch.empty(max(int(nbytes), 4) // 4 + 1, dtype=torch.float32, device=device)
+
+
+def version() -> str:
+    return LIB.ganamd_version().decode()

@@ -1,0 +1,481 @@
+// Memory-bound kernels of the WGAN-GP hot path for gfx950: train-mode BatchNorm fused with
+// PReLU, PReLU with its first and second derivatives, separable resampling (Smooth, bicubic,
+// adaptive average pooling and their adjoints), per-plane / per-row reductions and the fused
+// flat-buffer AdamW.  All activations are CNHW: a channel is one contiguous row of L = B*H*W.
+//
+// Reductions over a row are split over S blocks per channel so that a 64x64 feature map with
+// ~100 channels still launches thousands of workgroups; per-block partials go to caller-provided
+// workspace and a second tiny kernel merges them (no atomics: bitwise reproducible).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/ganamd.h"
+
+namespace {
+
+constexpr int kNT = 256;
+constexpr long kChunk = 4096;  // elements of a row per reduction block
+constexpr int kMaxSplit = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Sum over a 256-thread block; result valid in every thread.
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+inline int splits_for(long L) {
+  long s = (L + kChunk - 1) / kChunk;
+  if (s < 1) s = 1;
+  if (s > kMaxSplit) s = kMaxSplit;
+  return (int)s;
+}
+
+inline int grid_for(long n) {
+  long b = (n + kNT - 1) / kNT;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+// ---------------------------------------------------------------- BatchNorm statistics
+// block (s, c): chunk mean and M2 of row c (two passes over an L2-resident 16 KB chunk)
+__global__ __launch_bounds__(kNT) void bn_partial_kernel(const float* __restrict__ x, long L, int S,
+                                                         float* __restrict__ part) {
+  __shared__ float sh[4];
+  const int c = blockIdx.y, s = blockIdx.x;
+  const long per = (L + S - 1) / S;
+  const long lo = s * per, hi = min(L, lo + per);
+  const float* row = x + (long)c * L;
+  float acc = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) acc += row[i];
+  const float n = (float)max(0L, hi - lo);
+  const float mean = n > 0 ? block_sum(acc, sh) / n : 0.f;
+  float m2 = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    const float d = row[i] - mean;
+    m2 += d * d;
+  }
+  m2 = block_sum(m2, sh);
+  if (threadIdx.x == 0) {
+    float* o = part + ((long)c * S + s) * 3;
+    o[0] = n;
+    o[1] = mean;
+    o[2] = m2;
+  }
+}
+
+// Chan merge of the S partials, running-stat update, invstd.
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int C, int S, long L, float* running_mean,
+                                   float* running_var, float momentum, float eps, float* save_mean,
+                                   float* save_invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float* p = part + (long)c * S * 3;
+  double n = 0, mean = 0, m2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const double nb = p[3 * s], mb = p[3 * s + 1], m2b = p[3 * s + 2];
+    if (nb <= 0) continue;
+    const double nn = n + nb, d = mb - mean;
+    mean += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  const float var = (float)(m2 / (double)L);
+  save_mean[c] = (float)mean;
+  save_invstd[c] = 1.0f / sqrtf(var + eps);
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+  if (running_var) {
+    const float unb = L > 1 ? (float)(m2 / (double)(L - 1)) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  }
+}
+
+__global__ __launch_bounds__(kNT) void bn_act_apply_kernel(const float* __restrict__ x, int C, long L,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ alpha, float* __restrict__ y) {
+  const long total = (long)C * L;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < total; i += (long)gridDim.x * kNT) {
+    const int c = (int)(i / L);
+    float z = (x[i] - mean[c]) * invstd[c] * gamma[c] + beta[c];
+    if (alpha) z = z > 0.f ? z : alpha[c] * z;
+    y[i] = z;
+  }
+}
+
+// partial sums of g = gy*prelu'(z), g*xhat and gy*min(z,0)
+__global__ __launch_bounds__(kNT) void bn_act_bwd_partial_kernel(
+    const float* __restrict__ gy, const float* __restrict__ x, long L, int S, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ alpha, float* __restrict__ part) {
+  __shared__ float sh[4];
+  const int c = blockIdx.y, s = blockIdx.x;
+  const long per = (L + S - 1) / S;
+  const long lo = s * per, hi = min(L, lo + per);
+  const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c];
+  const float al = alpha ? alpha[c] : 1.f;
+  const float* xr = x + (long)c * L;
+  const float* gr = gy + (long)c * L;
+  float sg = 0.f, sgx = 0.f, sa = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    const float xh = (xr[i] - mu) * is;
+    const float gv = gr[i];
+    float g = gv;
+    if (alpha) {
+      const float z = xh * ga + be;
+      if (!(z > 0.f)) {
+        g = gv * al;
+        sa += gv * z;
+      }
+    }
+    sg += g;
+    sgx += g * xh;
+  }
+  sg = block_sum(sg, sh);
+  sgx = block_sum(sgx, sh);
+  sa = block_sum(sa, sh);
+  if (threadIdx.x == 0) {
+    float* o = part + ((long)blockIdx.y * S + s) * 3;
+    o[0] = sg;
+    o[1] = sgx;
+    o[2] = sa;
+  }
+}
+
+__global__ void reduce3_kernel(const float* __restrict__ part, int C, int S, float* o0, float* o1, float* o2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float* p = part + (long)c * S * 3;
+  float a = 0.f, b = 0.f, d = 0.f;
+  for (int s = 0; s < S; ++s) {
+    a += p[3 * s];
+    b += p[3 * s + 1];
+    d += p[3 * s + 2];
+  }
+  if (o0) o0[c] = a;
+  if (o1) o1[c] = b;
+  if (o2) o2[c] = d;
+}
+
+// gx = gamma*invstd*(g - sum(g)/L - xhat*sum(g*xhat)/L); the partial sums were reduced into
+// gbeta (= sum g) and ggamma (= sum g*xhat)
+__global__ __launch_bounds__(kNT) void bn_act_bwd_apply_kernel(
+    const float* __restrict__ gy, const float* __restrict__ x, int C, long L, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ alpha, const float* __restrict__ sum_g, const float* __restrict__ sum_gx,
+    float* __restrict__ gx) {
+  const long total = (long)C * L;
+  const float invL = 1.f / (float)L;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < total; i += (long)gridDim.x * kNT) {
+    const int c = (int)(i / L);
+    const float is = invstd[c];
+    const float xh = (x[i] - mean[c]) * is;
+    float g = gy[i];
+    if (alpha) {
+      const float z = xh * gamma[c] + beta[c];
+      if (!(z > 0.f)) g *= alpha[c];
+    }
+    gx[i] = gamma[c] * is * (g - sum_g[c] * invL - xh * sum_gx[c] * invL);
+  }
+}
+
+// ---------------------------------------------------------------- PReLU
+__global__ __launch_bounds__(kNT) void prelu_fwd_kernel(const float* __restrict__ x, const float* __restrict__ a,
+                                                        int C, long L, float* __restrict__ y) {
+  const long total = (long)C * L;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < total; i += (long)gridDim.x * kNT) {
+    const float v = x[i];
+    y[i] = v > 0.f ? v : a[i / L] * v;
+  }
+}
+
+// gx (optional) and per-block partials of galpha = sum gy*x over x<=0
+__global__ __launch_bounds__(kNT) void prelu_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                                                        const float* __restrict__ a, long L, int S,
+                                                        float* __restrict__ gx, float* __restrict__ part) {
+  __shared__ float sh[4];
+  const int c = blockIdx.y, s = blockIdx.x;
+  const long per = (L + S - 1) / S;
+  const long lo = s * per, hi = min(L, lo + per);
+  const float al = a[c];
+  const long base = (long)c * L;
+  float acc = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    const float v = x[base + i], g = gy[base + i];
+    if (v > 0.f) {
+      if (gx) gx[base + i] = g;
+    } else {
+      if (gx) gx[base + i] = al * g;
+      acc += g * v;
+    }
+  }
+  if (part) {
+    acc = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[(long)c * S + s] = acc;
+  }
+}
+
+__global__ __launch_bounds__(kNT) void prelu_bwd_bwd_kernel(const float* __restrict__ ggx,
+                                                            const float* __restrict__ gga,
+                                                            const float* __restrict__ gy, const float* __restrict__ x,
+                                                            const float* __restrict__ a, long L, int S,
+                                                            float* __restrict__ ggy, float* __restrict__ gx,
+                                                            float* __restrict__ part) {
+  __shared__ float sh[4];
+  const int c = blockIdx.y, s = blockIdx.x;
+  const long per = (L + S - 1) / S;
+  const long lo = s * per, hi = min(L, lo + per);
+  const float al = a[c];
+  const float ga = gga ? gga[c] : 0.f;
+  const long base = (long)c * L;
+  float acc = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    const float v = x[base + i];
+    const float gg = ggx ? ggx[base + i] : 0.f;
+    if (v > 0.f) {
+      if (ggy) ggy[base + i] = gg;
+      if (gx) gx[base + i] = 0.f;
+    } else {
+      const float g = gy[base + i];
+      if (ggy) ggy[base + i] = gg * al + ga * v;
+      if (gx) gx[base + i] = ga * g;
+      acc += gg * g;
+    }
+  }
+  if (part) {
+    acc = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[(long)c * S + s] = acc;
+  }
+}
+
+__global__ void reduce1_kernel(const float* __restrict__ part, int C, int S, float* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f;
+  for (int s = 0; s < S; ++s) a += part[(long)c * S + s];
+  out[c] = a;
+}
+
+// ---------------------------------------------------------------- row / plane reductions
+__global__ __launch_bounds__(kNT) void row_dot_kernel(const float* __restrict__ a, const float* __restrict__ b, long L,
+                                                      int S, float* __restrict__ part) {
+  __shared__ float sh[4];
+  const int c = blockIdx.y, s = blockIdx.x;
+  const long per = (L + S - 1) / S;
+  const long lo = s * per, hi = min(L, lo + per);
+  const long base = (long)c * L;
+  float acc = 0.f;
+  if (b) {
+    for (long i = lo + threadIdx.x; i < hi; i += kNT) acc += a[base + i] * b[base + i];
+  } else {
+    for (long i = lo + threadIdx.x; i < hi; i += kNT) acc += a[base + i];
+  }
+  acc = block_sum(acc, sh);
+  if (threadIdx.x == 0) part[(long)c * S + s] = acc;
+}
+
+// one wave per plane
+__global__ __launch_bounds__(kNT) void plane_dot_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                        long planes, long HW, float scale, float* __restrict__ out) {
+  const long wave = (blockIdx.x * (long)kNT + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * kNT) >> 6;
+  const int lane = threadIdx.x & 63;
+  for (long p = wave; p < planes; p += nwaves) {
+    const float* ap = a + p * HW;
+    float acc = 0.f;
+    if (b) {
+      const float* bp = b + p * HW;
+      for (long i = lane; i < HW; i += 64) acc += ap[i] * bp[i];
+    } else {
+      for (long i = lane; i < HW; i += 64) acc += ap[i];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) out[p] = scale * acc;
+  }
+}
+
+__global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int T, float* __restrict__ out) {
+  for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < rows; r += (long)gridDim.x * blockDim.x) {
+    const float* p = w + r * T;
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) acc += p[t] * p[t];
+    out[r] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- separable resampling
+__global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict__ x, long planes, int IH, int IW,
+                                                         float* __restrict__ y, int OH, int OW,
+                                                         const int32_t* __restrict__ ri, const float* __restrict__ rw,
+                                                         int KR, const int32_t* __restrict__ ci,
+                                                         const float* __restrict__ cw, int KC) {
+  const long total = planes * OH * OW;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < total; i += (long)gridDim.x * kNT) {
+    const int ow = (int)(i % OW);
+    const int oh = (int)((i / OW) % OH);
+    const long p = i / ((long)OH * OW);
+    const float* xp = x + p * IH * IW;
+    float acc = 0.f;
+    for (int a = 0; a < KR; ++a) {
+      const float wr = rw[oh * KR + a];
+      if (wr == 0.f) continue;
+      const float* xr = xp + (long)ri[oh * KR + a] * IW;
+      float racc = 0.f;
+      for (int b = 0; b < KC; ++b) racc += cw[ow * KC + b] * xr[ci[ow * KC + b]];
+      acc += wr * racc;
+    }
+    y[i] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- AdamW
+__global__ void step_increment_kernel(int32_t* step) { *step += 1; }
+
+__global__ __launch_bounds__(kNT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long n,
+                                                    const int32_t* __restrict__ step, float lr, float beta1,
+                                                    float beta2, float eps, float wd) {
+  const double t = (double)*step;
+  const float step_size = (float)((double)lr / (1.0 - pow((double)beta1, t)));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, t));
+  const float decay = (float)(1.0 - (double)lr * (double)wd);
+  const float w = 1.f - beta1;  // lerp weight
+  const float omb2 = 1.f - beta2;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < n; i += (long)gridDim.x * kNT) {
+    const float gi = g[i];
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = w < 0.5f ? mi + w * (gi - mi) : gi - (gi - mi) * (1.f - w);
+    float vi = v[i] * beta2 + omb2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi + (-step_size) * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+inline int ok(hipError_t e) { return e == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH; }
+
+}  // namespace
+
+extern "C" {
+
+const char* ganamd_version(void) { return "ganamd 0.1 gfx950"; }
+
+size_t ganamd_rowreduce_workspace(int C, long L) { return sizeof(float) * 3 * (size_t)C * splits_for(L); }
+
+int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
+                      float* running_mean, float* running_var, float momentum, float eps, float* y,
+                      float* save_mean, float* save_invstd, void* workspace, hipStream_t st) {
+  if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || C <= 0 || L <= 0)
+    return GANAMD_EINVAL;
+  const int S = splits_for(L);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(bn_partial_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, L, running_mean,
+                     running_var, momentum, eps, save_mean, save_invstd);
+  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, x, C, L, save_mean,
+                     save_invstd, gamma, beta, alpha, y);
+  return ok(hipGetLastError());
+}
+
+int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,
+                      const float* alpha, const float* save_mean, const float* save_invstd, float* gx, float* ggamma,
+                      float* gbeta, float* galpha, void* workspace, hipStream_t st) {
+  if (!gy || !x || !gamma || !beta || !save_mean || !save_invstd || !gx || !ggamma || !gbeta || !workspace)
+    return GANAMD_EINVAL;
+  const int S = splits_for(L);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(bn_act_bwd_partial_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, L, S, save_mean, save_invstd,
+                     gamma, beta, alpha, part);
+  hipLaunchKernelGGL(reduce3_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, gbeta, ggamma,
+                     alpha ? galpha : nullptr);
+  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, gy, x, C, L, save_mean,
+                     save_invstd, gamma, beta, alpha, gbeta, ggamma, gx);
+  return ok(hipGetLastError());
+}
+
+int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y, hipStream_t st) {
+  if (!x || !alpha || !y || C <= 0 || L <= 0) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(prelu_fwd_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, x, alpha, C, L, y);
+  return ok(hipGetLastError());
+}
+
+int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C, long L, float* gx, float* galpha,
+                     void* workspace, hipStream_t st) {
+  if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
+  const int S = splits_for(L);
+  float* part = galpha ? static_cast<float*>(workspace) : nullptr;
+  hipLaunchKernelGGL(prelu_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, alpha, L, S, gx, part);
+  if (galpha) hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha);
+  return ok(hipGetLastError());
+}
+
+int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy, const float* x, const float* alpha,
+                         int C, long L, float* ggy, float* gx, float* galpha, void* workspace, hipStream_t st) {
+  if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
+  const int S = splits_for(L);
+  float* part = galpha ? static_cast<float*>(workspace) : nullptr;
+  hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, ggx, ggalpha, gy, x, alpha, L, S, ggy, gx,
+                     part);
+  if (galpha) hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha);
+  return ok(hipGetLastError());
+}
+
+int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
+                      const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t st) {
+  if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(resample2d_kernel, dim3(grid_for(planes * OH * OW)), dim3(kNT), 0, st, x, planes, IH, IW, y, OH,
+                     OW, ri, rw, KR, ci, cw, KC);
+  return ok(hipGetLastError());
+}
+
+int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float scale, float* out, hipStream_t st) {
+  if (!a || !out || planes <= 0 || HW <= 0) return GANAMD_EINVAL;
+  const long waves = planes;
+  int blocks = (int)std::min<long>((waves + 3) / 4, 16384);
+  hipLaunchKernelGGL(plane_dot_kernel, dim3(blocks), dim3(kNT), 0, st, a, b, planes, HW, scale, out);
+  return ok(hipGetLastError());
+}
+
+int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, void* workspace, hipStream_t st) {
+  if (!a || !out || !workspace || C <= 0 || L <= 0) return GANAMD_EINVAL;
+  const int S = splits_for(L);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(row_dot_kernel, dim3(S, C), dim3(kNT), 0, st, a, b, L, S, part);
+  hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, out);
+  return ok(hipGetLastError());
+}
+
+int ganamd_segment_sumsq(const float* w, long rows, int T, float* out, hipStream_t st) {
+  if (!w || !out || rows <= 0 || T <= 0) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(segment_sumsq_kernel, dim3(grid_for(rows)), dim3(kNT), 0, st, w, rows, T, out);
+  return ok(hipGetLastError());
+}
+
+int ganamd_adamw(float* p, const float* g, float* m, float* v, long n, int32_t* step, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, hipStream_t st) {
+  if (!p || !g || !m || !v || !step || n <= 0) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(step_increment_kernel, dim3(1), dim3(1), 0, st, step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(kNT), 0, st, p, g, m, v, n, step, lr, beta1, beta2, eps,
+                     weight_decay);
+  return ok(hipGetLastError());
+}
+
+}  // extern "C"

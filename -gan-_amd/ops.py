@@ -1,0 +1,408 @@
+"""Autograd operators of the hot path, each backed by libganamd.so kernels.
+
+Tensors are CNHW: a feature map is [C, B, H, W]; a per-sample feature vector (linear layers,
+styles, SE/SK attention) is [C, B].
+
+Closure under differentiation.  The critic's gradient penalty calls
+``autograd.grad(create_graph=True)`` and then ``backward()`` through it (wgangp.py:45-54,69),
+so every operator the critic uses has a backward made of differentiable operators:
+  conv forward / dgrad / wgrad        -> each other's backward (bilinear family)
+  PReLU  -> PReLUBackward -> prelu double-backward kernel
+  resample (smooth, bicubic, pools)   -> the same kernel with the transposed tap table
+Generator-only operators (fused BatchNorm+PReLU, the modulated conv) are first-order.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from . import _lib
+from ._lib import LIB, check, iptr, ptr, stream, workspace
+from . import tables
+
+# ------------------------------------------------------------------------------------------
+# convolution geometry
+# ------------------------------------------------------------------------------------------
+
+
+@dataclass(frozen=True)
+class Geo:
+    B: int
+    Cin: int
+    H: int
+    W: int
+    Cout: int
+    OH: int
+    OW: int
+    K: int
+    stride: int = 1
+    pad: int = 0
+    pad_mode: int = _lib.PAD_REPLICATE
+    transposed: bool = False
+
+    def desc(self):
+        d = _DESC_CACHE.get(self)
+        if d is None:
+            d = _lib.ConvDesc(self.B, self.Cin, self.H, self.W, self.Cout, self.OH, self.OW, self.K, self.K,
+                              self.stride, self.pad, self.pad_mode, int(self.transposed))
+            _DESC_CACHE[self] = d
+        return d
+
+    def ws_bytes(self, op):
+        n = _lib.c_size_t(0)
+        check(LIB.ganamd_conv_workspace(self.desc(), op, n), "conv_workspace")
+        return n.value
+
+
+_DESC_CACHE: dict = {}
+
+
+def conv_geo(B, cin, h, w, cout, k, stride=1, pad=0, pad_mode=_lib.PAD_REPLICATE):
+    oh = (h + 2 * pad - k) // stride + 1
+    ow = (w + 2 * pad - k) // stride + 1
+    return Geo(B, cin, h, w, cout, oh, ow, k, stride, pad, pad_mode, False)
+
+
+def convT_geo(B, cin, h, w, cout, k, stride, pad):
+    oh = (h - 1) * stride - 2 * pad + k
+    ow = (w - 1) * stride - 2 * pad + k
+    return Geo(B, cin, h, w, cout, oh, ow, k, stride, pad, _lib.PAD_ZERO, True)
+
+
+def linear_geo(B, cin, cout):
+    return Geo(B, cin, 1, 1, cout, 1, 1, 1, 1, 0, _lib.PAD_ZERO, False)
+
+
+def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0):
+    y = torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device, dtype=torch.float32)
+    check(LIB.ganamd_conv_fwd(geo.desc(), ptr(x), ptr(w), ptr(bias), ptr(xs), ptr(ys), float(alpha), ptr(y),
+                              stream()), "conv_fwd")
+    return y
+
+
+def _conv_dgrad(geo: Geo, gy, w, gys=None, alpha=1.0):
+    gx = torch.empty((geo.Cin, geo.B, geo.H, geo.W), device=gy.device, dtype=torch.float32)
+    nb = geo.ws_bytes(_lib.CONV_DGRAD)
+    ws = workspace(nb, gy.device) if nb else None
+    check(LIB.ganamd_conv_dgrad(geo.desc(), ptr(gy), ptr(w), ptr(gys), float(alpha), ptr(gx), ptr(ws), stream()),
+          "conv_dgrad")
+    return gx
+
+
+def _conv_wgrad(geo: Geo, x, gy, xs=None, gys=None, alpha=1.0, out=None, accumulate=False):
+    shape = (geo.Cin, geo.Cout, geo.K, geo.K) if geo.transposed else (geo.Cout, geo.Cin, geo.K, geo.K)
+    gw = out if out is not None else torch.empty(shape, device=x.device, dtype=torch.float32)
+    check(LIB.ganamd_conv_wgrad(geo.desc(), ptr(x), ptr(gy), ptr(xs), ptr(gys), float(alpha), ptr(gw),
+                                int(accumulate), stream()), "conv_wgrad")
+    return gw
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+class ConvFwd(Function):
+    """y = alpha * conv(x, w) + bias   (any order of derivative)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, geo, alpha):
+        x, w = _c(x), _c(w)
+        ctx.save_for_backward(x, w)
+        ctx.geo, ctx.alpha, ctx.has_bias = geo, alpha, bias is not None
+        return _conv_fwd(geo, x, w, None if bias is None else _c(bias), alpha=alpha)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        geo, alpha = ctx.geo, ctx.alpha
+        gx = ConvDgrad.apply(gy, w, geo, alpha) if ctx.needs_input_grad[0] else None
+        gw = ConvWgrad.apply(x, gy, geo, alpha) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(dim=(1, 2, 3)) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        return gx, gw, gb, None, None
+
+
+class ConvDgrad(Function):
+    """gx = alpha * conv^T(gy, w)."""
+
+    @staticmethod
+    def forward(ctx, gy, w, geo, alpha):
+        gy, w = _c(gy), _c(w)
+        ctx.save_for_backward(gy, w)
+        ctx.geo, ctx.alpha = geo, alpha
+        return _conv_dgrad(geo, gy, w, alpha=alpha)
+
+    @staticmethod
+    def backward(ctx, ggx):
+        gy, w = ctx.saved_tensors
+        geo, alpha = ctx.geo, ctx.alpha
+        g_gy = ConvFwd.apply(ggx, w, None, geo, alpha) if ctx.needs_input_grad[0] else None
+        g_w = ConvWgrad.apply(ggx, gy, geo, alpha) if ctx.needs_input_grad[1] else None
+        return g_gy, g_w, None, None
+
+
+class ConvWgrad(Function):
+    """gw = alpha * d<gy, conv(x, w)>/dw."""
+
+    @staticmethod
+    def forward(ctx, x, gy, geo, alpha):
+        x, gy = _c(x), _c(gy)
+        ctx.save_for_backward(x, gy)
+        ctx.geo, ctx.alpha = geo, alpha
+        return _conv_wgrad(geo, x, gy, alpha=alpha)
+
+    @staticmethod
+    def backward(ctx, ggw):
+        x, gy = ctx.saved_tensors
+        geo, alpha = ctx.geo, ctx.alpha
+        g_x = ConvDgrad.apply(gy, ggw, geo, alpha) if ctx.needs_input_grad[0] else None
+        g_gy = ConvFwd.apply(x, ggw, None, geo, alpha) if ctx.needs_input_grad[1] else None
+        return g_x, g_gy, None, None
+
+
+def conv2d(x, w, bias, geo: Geo, alpha: float):
+    return ConvFwd.apply(x, w, bias, geo, alpha)
+
+
+def linear(x, w, bias, alpha: float):
+    """EqualizedLinear on [Cin, B] -> [Cout, B] (a 1x1 conv at H = W = 1)."""
+    cin, B = x.shape
+    cout = w.shape[0]
+    geo = linear_geo(B, cin, cout)
+    return ConvFwd.apply(x.reshape(cin, B, 1, 1), w.reshape(cout, cin, 1, 1), bias, geo, alpha).reshape(cout, B)
+
+
+# ------------------------------------------------------------------------------------------
+# PReLU (twice differentiable)
+# ------------------------------------------------------------------------------------------
+
+
+def _rows(x):
+    C = x.shape[0]
+    return C, x.numel() // C
+
+
+class PReLU(Function):
+    @staticmethod
+    def forward(ctx, x, a):
+        x = _c(x)
+        C, L = _rows(x)
+        y = torch.empty_like(x)
+        check(LIB.ganamd_prelu_fwd(ptr(x), ptr(a), C, L, ptr(y), stream()), "prelu_fwd")
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, a = ctx.saved_tensors
+        gx, ga = PReLUBackward.apply(gy, x, a)
+        return gx, ga
+
+
+class PReLUBackward(Function):
+    @staticmethod
+    def forward(ctx, gy, x, a):
+        gy = _c(gy)
+        C, L = _rows(x)
+        gx = torch.empty_like(x)
+        ga = torch.empty_like(a)
+        ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
+        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), ptr(ga), ptr(ws), stream()), "prelu_bwd")
+        ctx.save_for_backward(gy, x, a)
+        return gx, ga
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, ggx, gga):
+        gy, x, a = ctx.saved_tensors
+        C, L = _rows(x)
+        ggx = None if ggx is None else _c(ggx)
+        gga = None if gga is None else _c(gga)
+        need_gy, need_x, need_a = ctx.needs_input_grad
+        g_gy = torch.empty_like(x) if need_gy else None
+        g_x = torch.empty_like(x) if (need_x and gga is not None) else None
+        g_a = torch.empty_like(a) if need_a else None
+        if g_gy is None and g_x is None and g_a is None:
+            return None, None, None
+        ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
+        check(LIB.ganamd_prelu_bwd_bwd(ptr(ggx), ptr(gga), ptr(gy), ptr(x), ptr(a), C, L, ptr(g_gy), ptr(g_x),
+                                       ptr(g_a), ptr(ws), stream()), "prelu_bwd_bwd")
+        return g_gy, g_x, g_a
+
+
+def prelu(x, a):
+    return PReLU.apply(x, a)
+
+
+# ------------------------------------------------------------------------------------------
+# BatchNorm (train mode) fused with an optional PReLU -- generator only (first order)
+# ------------------------------------------------------------------------------------------
+
+
+class BNAct(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, alpha, running_mean, running_var, momentum, eps):
+        x = _c(x)
+        C, L = _rows(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
+        check(LIB.ganamd_bn_act_fwd(ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(running_mean),
+                                    ptr(running_var), float(momentum), float(eps), ptr(y), ptr(mean), ptr(invstd),
+                                    ptr(ws), stream()), "bn_act_fwd")
+        ctx.save_for_backward(x, gamma, beta, alpha, mean, invstd)
+        ctx.has_alpha = alpha is not None
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        x, gamma, beta, alpha, mean, invstd = ctx.saved_tensors
+        gy = _c(gy)
+        C, L = _rows(x)
+        gx = torch.empty_like(x)
+        gg = torch.empty_like(gamma)
+        gb = torch.empty_like(beta)
+        ga = torch.empty_like(alpha) if ctx.has_alpha else None
+        ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
+        check(LIB.ganamd_bn_act_bwd(ptr(gy), ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(mean), ptr(invstd),
+                                    ptr(gx), ptr(gg), ptr(gb), ptr(ga), ptr(ws), stream()), "bn_act_bwd")
+        return gx, gg, gb, ga, None, None, None, None
+
+
+def bn_act(x, bn: torch.nn.modules.batchnorm._BatchNorm, act: torch.nn.PReLU | None = None):
+    """Train-mode ``act(bn(x))`` with the module's parameters and running buffers."""
+    return BNAct.apply(x, bn.weight, bn.bias, None if act is None else act.weight, bn.running_mean, bn.running_var,
+                       bn.momentum, bn.eps)
+
+
+# ------------------------------------------------------------------------------------------
+# separable resampling (linear; its backward is the same kernel with the adjoint table)
+# ------------------------------------------------------------------------------------------
+
+
+def _resample(x, n_in, n_out, tab):
+    idx, w, k = tab
+    C, B = x.shape[0], x.shape[1]
+    y = torch.empty((C, B, n_out, n_out), device=x.device, dtype=torch.float32)
+    check(LIB.ganamd_resample2d(ptr(x), C * B, n_in, n_in, ptr(y), n_out, n_out, iptr(idx), ptr(w), k, iptr(idx),
+                                ptr(w), k, stream()), "resample2d")
+    return y
+
+
+class Resample(Function):
+    @staticmethod
+    def forward(ctx, x, table, adjoint):
+        ctx.table, ctx.adjoint = table, adjoint
+        if adjoint:
+            return _resample(_c(x), table.n_out, table.n_in, table.adj)
+        return _resample(_c(x), table.n_in, table.n_out, table.fwd)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return Resample.apply(gy, ctx.table, not ctx.adjoint), None, None
+
+
+def resample(x, kind: str):
+    return Resample.apply(x, tables.table(kind, x.shape[2], x.device), False)
+
+
+# ------------------------------------------------------------------------------------------
+# per-plane mean (AdaptiveAvgPool2d(1)) -> [C, B]
+# ------------------------------------------------------------------------------------------
+
+
+class PlaneMean(Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x)
+        C, B, H, W = x.shape
+        out = torch.empty((C, B), device=x.device, dtype=torch.float32)
+        check(LIB.ganamd_plane_dot(ptr(x), None, C * B, H * W, 1.0 / (H * W), ptr(out), stream()), "plane_dot")
+        ctx.hw = (H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        H, W = ctx.hw
+        return (g / (H * W))[:, :, None, None].expand(-1, -1, H, W)
+
+
+def plane_mean(x):
+    if x.shape[2] == 1 and x.shape[3] == 1:
+        return x.reshape(x.shape[0], x.shape[1])
+    return PlaneMean.apply(x)
+
+
+def plane_dot(a, b, scale=1.0):
+    a, b = _c(a), _c(b)
+    C, B, H, W = a.shape
+    out = torch.empty((C, B), device=a.device, dtype=torch.float32)
+    check(LIB.ganamd_plane_dot(ptr(a), ptr(b), C * B, H * W, float(scale), ptr(out), stream()), "plane_dot")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# weight-modulated conv (StyleGAN2 demodulation) -- generator only
+# ------------------------------------------------------------------------------------------
+
+
+class ModConv(Function):
+    """y[co,b] = c * d[co,b] * conv(x * s[ci,b], W)   (generator_13_5.py:234-248, batch-shared form).
+
+    ``d`` is an input (computed by ``demod`` with differentiable ops) so that autograd carries
+    its gradient back into s and W.
+    """
+
+    @staticmethod
+    def forward(ctx, x, s, d, w, geo, c):
+        x, s, d, w = _c(x), _c(s), _c(d), _c(w)
+        y = _conv_fwd(geo, x, w, None, s, d, c)
+        ctx.save_for_backward(x, s, d, w, y)
+        ctx.geo, ctx.c = geo, c
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        x, s, d, w, y = ctx.saved_tensors
+        geo, c = ctx.geo, ctx.c
+        gy = _c(gy)
+        gx = gs = gd = gw = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            gxs = _conv_dgrad(geo, gy, w, d, c)             # d/d(x*s)
+            if ctx.needs_input_grad[0]:
+                gx = gxs * s[:, :, None, None]
+            if ctx.needs_input_grad[1]:
+                gs = plane_dot(gxs, x)
+        if ctx.needs_input_grad[2]:
+            gd = plane_dot(gy, y) / d                       # y = d * conv  =>  dL/dd = sum gy*conv
+        if ctx.needs_input_grad[3]:
+            gw = _conv_wgrad(geo, x, gy, s, d, c)
+        return gx, gs, gd, gw, None, None
+
+
+def demod(s, w, c, eps=1e-8):
+    """d[co,b] = rsqrt(c^2 * sum_ci s[ci,b]^2 * sum_k W[co,ci,k]^2 + eps)."""
+    wsq = w.pow(2).sum(dim=(2, 3))                       # [Cout, Cin]
+    return torch.rsqrt((c * c) * (wsq @ (s * s)) + eps)  # [Cout, B]
+
+
+def modconv(x, s, w, geo, c):
+    return ModConv.apply(x, s, demod(s, w, c), w, geo, c)
+
+
+# ------------------------------------------------------------------------------------------
+# layout helpers at the module boundary
+# ------------------------------------------------------------------------------------------
+
+
+def nchw_to_cnhw(x):
+    return x.permute(1, 0, 2, 3).contiguous()
+
+
+def cnhw_to_nchw(x):
+    return x.permute(1, 0, 2, 3).contiguous()

@@ -1,0 +1,116 @@
+"""Drop-in WGAN-GP trainer (reference: train/wgangp.py ``Train``).
+
+Same step semantics as train/wgangp.py:20-71: zero_grad placement, the generator forward under
+``no_grad`` in the critic step, real/fake critic losses with separate ``backward()`` calls, the
+gradient penalty on eps-interpolated samples with ``autograd.grad(create_graph=True)`` and
+lambda = 10, ``sqrt`` then ``- center``, batch mean, AdamW (G lr 1e-4, D lr 4e-4, betas
+(0.5, 0.999)).
+
+Differences that do not change what is trained:
+  * AdamW is the fused flat-buffer kernel (optim.py).
+  * The critic's input gradient on the fake batch (left in ``gen_imgs.grad`` by
+    wgangp.py:65-67 and never read) is not computed.
+  * In the generator step the critic's parameters are frozen for the backward: the reference
+    computes D's weight gradients there and throws them away at the next critic zero_grad
+    ("dead D wgrad"); we do not compute them.
+  * Randomness comes from a pluggable source (rng.py) so runs can replay a seeded sequence.
+  * The GUI / image-grid / checkpoint side work of train/trainunits.py is not part of the hot
+    path; ``train()`` runs the step loop only.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from .optim import FusedAdamW
+from .rng import DeviceRNG
+
+
+@contextlib.contextmanager
+def _frozen(module):
+    ps = [p for p in module.parameters() if p.requires_grad]
+    for p in ps:
+        p.requires_grad_(False)
+    try:
+        yield
+    finally:
+        for p in ps:
+            p.requires_grad_(True)
+
+
+class Train:
+    def __init__(self, dataloader, device, num_epochs, nz, generator, generator_name, discriminator,
+                 discriminator_name, rng=None):
+        self.dataloader = dataloader
+        self.device = torch.device(device)
+        self.num_epochs = num_epochs
+        self.nz = nz
+        self.generator, self.generator_name = generator, generator_name
+        self.discriminator, self.discriminator_name = discriminator, discriminator_name
+        self.rng = rng if rng is not None else DeviceRNG(self.device)
+        self.optimizer_G = FusedAdamW(generator, lr=0.0001, betas=(0.5, 0.999))
+        self.optimizer_D = FusedAdamW(discriminator, lr=0.0004, betas=(0.5, 0.999))
+
+    def _generate(self, z):
+        self.generator.noise_hub.source = self.rng.noise
+        return self.generator(z)
+
+    def generator_trainstep(self, b_size):
+        """train/wgangp.py:20-27."""
+        self.optimizer_G.zero_grad()
+        z = self.rng.randn((b_size, self.nz, 1, 1))
+        gen_imgs = self._generate(z)
+        with _frozen(self.discriminator):
+            g_loss = -torch.mean(self.discriminator(gen_imgs))
+            g_loss.backward()
+        self.optimizer_G.step()
+        return gen_imgs, g_loss
+
+    def discriminator_loss(self, real_pred, fake_pred):
+        return torch.mean(fake_pred) - torch.mean(real_pred)
+
+    def gradient_penalty(self, x_real, x_fake, batch_size, device=None, center=1.0):
+        """train/wgangp.py:34-43."""
+        eps = self.rng.rand((batch_size,)).view(batch_size, 1, 1, 1)
+        x_interp = ((1 - eps) * x_real + eps * x_fake).detach()
+        x_interp.requires_grad_()
+        d_out = self.discriminator(x_interp)
+        return (self.compute_grad2(d_out, x_interp).sqrt() - center).pow(2).mean()
+
+    def compute_grad2(self, d_out, x_in):
+        """train/wgangp.py:45-54."""
+        batch_size = x_in.size(0)
+        grad_dout = torch.autograd.grad(outputs=d_out.sum(), inputs=x_in, create_graph=True, retain_graph=True,
+                                        only_inputs=True)[0]
+        grad_dout2 = grad_dout.pow(2)
+        assert grad_dout2.size() == x_in.size()
+        return grad_dout2.view(batch_size, -1).sum(1)
+
+    def discriminator_trainstep(self, images, b_size):
+        """train/wgangp.py:56-71."""
+        self.optimizer_D.zero_grad()
+        z = self.rng.randn((b_size, self.nz, 1, 1))
+        with torch.no_grad():
+            gen_imgs = self._generate(z)
+        gen_imgs.requires_grad_()
+        pred_r = self.discriminator(images)
+        real_loss = -torch.mean(pred_r)
+        real_loss.backward()
+        # the input gradient this backward would leave in gen_imgs.grad is never read (dead work)
+        pred_f = self.discriminator(gen_imgs.detach())
+        fake_loss = torch.mean(pred_f)
+        fake_loss.backward()
+        gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
+        gp.backward()
+        self.optimizer_D.step()
+        return real_loss, fake_loss, gp
+
+    def train(self):
+        """Epoch loop of train/wgangp.py:73-95 without the display / checkpoint side work."""
+        for _epoch in range(self.num_epochs):
+            for images, _ in self.dataloader:
+                images = images.to(self.device)
+                b = images.shape[0]
+                self.discriminator_trainstep(images, b)
+                self.generator_trainstep(b)

@@ -1,0 +1,152 @@
+/*
+ * ganamd.h — C ABI of the MI355X-native WGAN-GP hot path (G13_5 + D9_4), libganamd.so.
+ *
+ * The reference has no FFI: its hot path sits behind PyTorch's nn.Module + autograd protocol
+ * (SURVEY.md §8(b)).  Each entry point below replaces the ATen kernel(s) that the reference's
+ * modules reach through that protocol; the file:line of the reference call site is cited per
+ * function.  The drop-in Python modules (-gan-_amd/) call these through ctypes.
+ *
+ * Conventions
+ *   - Activations are fp32 in CNHW layout ("channel rows"): x[c][b][h][w], row length
+ *     L = B*H*W.  A vector indexed by (channel, sample), e.g. a style or a demodulation
+ *     coefficient, is stored [C][B].
+ *   - All pointers are device pointers; every call is asynchronous on `stream` and performs no
+ *     allocation and no host synchronisation (safe under hipGraph stream capture).
+ *   - Scratch memory is caller-provided; query its size with the *_workspace functions.
+ *   - Return 0 (GANAMD_OK) or a negative error code.  No exceptions cross the ABI.
+ *   - Stateless: calls on distinct streams may run concurrently from several threads.
+ */
+#ifndef GANAMD_H
+#define GANAMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GANAMD_OK 0
+#define GANAMD_EINVAL (-1)
+#define GANAMD_ELAUNCH (-2)
+
+#define GANAMD_PAD_ZERO 0
+#define GANAMD_PAD_REPLICATE 1
+
+#define GANAMD_CONV_FWD 0
+#define GANAMD_CONV_DGRAD 1
+#define GANAMD_CONV_WGRAD 2
+
+/* Geometry of one convolution.  For transposed=0 the weight is [Cout][Cin][KH][KW] and
+ * OH = (H + 2*pad - KH)/stride + 1.  For transposed=1 (nn.ConvTranspose2d semantics, zero
+ * padding) the weight is [Cin][Cout][KH][KW] and OH = (H-1)*stride - 2*pad + KH.  A linear
+ * layer is the case H = W = OH = OW = KH = KW = 1. */
+typedef struct ganamd_conv_desc {
+  int32_t B, Cin, H, W;
+  int32_t Cout, OH, OW;
+  int32_t KH, KW, stride, pad;
+  int32_t pad_mode;   /* GANAMD_PAD_ZERO | GANAMD_PAD_REPLICATE (ignored when transposed) */
+  int32_t transposed;
+} ganamd_conv_desc;
+
+/* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD). */
+int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
+
+/* y[co][b,oh,ow] = alpha * y_scale[co][b] * sum W * (x * x_scale[ci][b]) + bias[co]
+ * Replaces: EqualizedConv2d.forward = F.conv2d(ReplicationPad2d(x), W*c, b)
+ *   (generator_13_5.py:36-38, discriminator_9_4.py:38-40); Conv2dWeightModulate.forward's
+ *   grouped conv with per-sample weights W*c*s*d (generator_13_5.py:234-248) via x_scale = s,
+ *   y_scale = d; nn.ConvTranspose2d (generator_13_5.py:156,594) with transposed=1;
+ *   EqualizedLinear = F.linear (generator_13_5.py:25-26, discriminator_9_4.py:26-27).
+ * x_scale, y_scale, bias may be NULL. */
+int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
+                    const float* x_scale, const float* y_scale, float alpha, float* y, hipStream_t stream);
+
+/* gx = alpha * dConv/dx applied to (gy * gy_scale[co][b]), including the ReplicationPad2d
+ * backward (edge folding).  Replaces aten convolution_backward (input grad) + replication_pad2d_backward.
+ * Workspace: ganamd_conv_workspace(d, GANAMD_CONV_DGRAD). */
+int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale,
+                      float alpha, float* gx, void* workspace, hipStream_t stream);
+
+/* gw (+)= alpha * dConv/dW for inputs (x * x_scale) and (gy * gy_scale).  accumulate=0
+ * overwrites gw.  Replaces aten convolution_backward (weight grad). */
+int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
+                      const float* gy_scale, float alpha, float* gw, int accumulate, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Train-mode BatchNorm (1d or 2d) fused with an optional per-channel PReLU.
+ * Replaces nn.BatchNorm2d/1d -> nn.PReLU pairs (generator_13_5.py:166,196,211-212,48-49,...).
+ * x, y: [C][L].  alpha may be NULL (no activation).  running_* may be NULL.
+ * save_mean / save_invstd: [C] outputs kept for the backward.
+ * Workspace: ganamd_rowreduce_workspace(C, L).
+ * ------------------------------------------------------------------------------------- */
+size_t ganamd_rowreduce_workspace(int C, long L);
+
+int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
+                      float* running_mean, float* running_var, float momentum, float eps, float* y,
+                      float* save_mean, float* save_invstd, void* workspace, hipStream_t stream);
+
+/* Backward of ganamd_bn_act_fwd: writes gx [C][L], ggamma, gbeta, galpha ([C]; galpha may be
+ * NULL when alpha is NULL). */
+int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,
+                      const float* alpha, const float* save_mean, const float* save_invstd, float* gx,
+                      float* ggamma, float* gbeta, float* galpha, void* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * PReLU (per-channel slope) with first and second derivatives (nn.PReLU; the critic's
+ * gradient penalty differentiates through its backward: wgangp.py:47-50,69).
+ * ------------------------------------------------------------------------------------- */
+int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y, hipStream_t stream);
+/* gx = gy * (x>0 ? 1 : alpha); galpha[c] = sum gy*x over x<=0 */
+int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C, long L, float* gx, float* galpha,
+                     void* workspace, hipStream_t stream);
+/* Backward of ganamd_prelu_bwd given ggx = dR/dgx and ggalpha = dR/dgalpha (may be NULL):
+ *   ggy = ggx*(x>0?1:alpha) + ggalpha[c]*(x>0?0:x)
+ *   gx  = ggalpha[c]*gy*(x>0?0:1)            (may be NULL)
+ *   galpha[c] = sum ggx*gy over x<=0         (may be NULL) */
+int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy, const float* x, const float* alpha,
+                         int C, long L, float* ggy, float* gx, float* galpha, void* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Separable 2-D resampling with per-axis tap tables (ELL format, K taps per output index):
+ *   y[p][oh][ow] = sum_i sum_j rw[oh][i] * cw[ow][j] * x[p][ri[oh][i]][ci[ow][j]]
+ * Covers Smooth (binomial 3x3, replication pad; generator_13_5.py:134-150,
+ * discriminator_9_4.py:56-72), bicubic x2 / x1/2 with A=-0.75 and clamped taps
+ * (generator_13_5.py:160, discriminator_9_4.py:81), AdaptiveAvgPool2d(5)
+ * (generator_13_5.py:44,355; discriminator_9_4.py:86), their compositions and, with the
+ * transposed tables, their adjoints (backward).
+ * ------------------------------------------------------------------------------------- */
+int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
+                      const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t stream);
+
+/* out[p] = scale * sum_{hw} a[p][hw] * (b ? b[p][hw] : 1)   (planes of HW elements).
+ * Replaces AdaptiveAvgPool2d(1) (generator_13_5.py:52,362) and the per-(channel,sample)
+ * reductions of the modulated-conv / SK / SE backward. */
+int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float scale, float* out,
+                     hipStream_t stream);
+
+/* out[c] = sum_{l} a[c][l] * (b ? b[c][l] : 1) over rows of length L. */
+int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, void* workspace, hipStream_t stream);
+
+/* out[i] = sum_{t<T} w[i*T + t]^2  (row sums of squares; the demodulation norm's sum over taps) */
+int ganamd_segment_sumsq(const float* w, long rows, int T, float* out, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused AdamW over one flat fp32 buffer (torch.optim.AdamW as configured at wgangp.py:17-18):
+ *   step += 1 (device counter, so a captured graph replays correctly)
+ *   p *= 1 - lr*wd; m = lerp(m, g, 1-beta1); v = beta2*v + (1-beta2)*g*g
+ *   p -= lr/(1-beta1^t) * m / (sqrt(v)/sqrt(1-beta2^t) + eps)
+ * ------------------------------------------------------------------------------------- */
+int ganamd_adamw(float* p, const float* g, float* m, float* v, long n, int32_t* step, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, hipStream_t stream);
+
+/* Library identification (for load checks). */
+const char* ganamd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GANAMD_H */

@@ -71,3 +71,17 @@ def grad_norm_stats(got, want, floor_frac=1e-6):
     e = np.abs(g - w) / np.abs(w)
     vec = float(np.linalg.norm(g - w) / np.linalg.norm(w))
     return float(np.median(e)), float(np.percentile(e, 99)), float(e.max()), vec
+
+
+# Step-level gradient bars (see grad_norm_stats for why they are norm-based).
+# D-step: GP double backward; G-step: ~100 sequential BN layers at B=4 (BN1d over 4 samples
+# amplifies rounding where a feature is nearly constant across the batch).
+D_BAR = dict(median=2e-4, p99=2e-3, max=2e-2, vec=1e-3)
+G_BAR = dict(median=2e-4, p99=5e-3, max=1e-1, vec=1e-3)
+
+
+def check_grads(rows, want, bar):
+    med, p99, mx, vec = grad_norm_stats(rows, want)
+    assert med < bar["median"] and p99 < bar["p99"], (med, p99, mx, vec)
+    assert mx < bar["max"] and vec < bar["vec"], (med, p99, mx, vec)
+    return med, p99, mx, vec

@@ -1,0 +1,293 @@
+"""GPU: every libganamd kernel against a float64 PyTorch-CPU restatement of the same op.
+
+Layout: our ops take CNHW; the references are written NCHW and permuted.  Tolerance: 1e-4
+norm-relative (fp32 MFMA / fp32 reductions against float64)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def cn(x):  # NCHW cpu -> CNHW gpu fp32
+    return x.detach().permute(1, 0, 2, 3).contiguous().float().to(DEV)
+
+
+def nc(x):  # CNHW gpu -> NCHW cpu double
+    return x.permute(1, 0, 2, 3).double().cpu()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import gan_amd.ops as o
+    return o
+
+
+def ref_conv(x, w, b, k, stride, pad, mode):
+    if pad:
+        x = F.pad(x, (pad,) * 4, mode="replicate" if mode == 1 else "constant")
+    return F.conv2d(x, w, b, stride=stride)
+
+
+CONV_CASES = [
+    # B, Cin, H, Cout, k, stride, pad, mode
+    (4, 5, 8, 7, 3, 1, 1, 1),
+    (2, 48, 16, 48, 5, 1, 2, 1),
+    (4, 16, 8, 33, 3, 2, 1, 1),
+    (3, 20, 5, 20, 3, 1, 0, 0),
+    (4, 17, 6, 9, 1, 1, 0, 0),
+    (4, 64, 8, 200, 3, 1, 1, 1),
+    (2, 130, 4, 260, 3, 1, 1, 1),
+    (8, 3, 64, 64, 3, 1, 1, 1),
+    (4, 96, 32, 96, 5, 1, 2, 1),
+    (4, 1025, 4, 1025, 3, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(ops, case):
+    B, Cin, H, Cout, k, s, p, mode = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64, requires_grad=True)
+    alpha = 0.37
+    y = ref_conv(x, w * alpha, b, k, s, p, mode)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    gx, gw, gb = torch.autograd.grad(y, (x, w, b), gy)
+
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, s, p, mode)
+    assert (geo.OH, geo.OW) == tuple(y.shape[2:])
+    xg, wg, bg = cn(x), w.detach().float().to(DEV), b.detach().float().to(DEV)
+    yg = ops._conv_fwd(geo, xg, wg, bg, alpha=alpha)
+    assert rel(nc(yg), y) < 1e-4
+    gyg = cn(gy)
+    assert rel(nc(ops._conv_dgrad(geo, gyg, wg, alpha=alpha)), gx) < 1e-4
+    assert rel(ops._conv_wgrad(geo, xg, gyg, alpha=alpha), gw) < 1e-4
+    # through autograd (bias grad included)
+    xa = xg.clone().requires_grad_()
+    wa = wg.clone().requires_grad_()
+    ba = bg.clone().requires_grad_()
+    ya = ops.conv2d(xa, wa, ba, geo, alpha)
+    ya.backward(gyg)
+    assert rel(nc(xa.grad), gx) < 1e-4 and rel(wa.grad, gw) < 1e-4 and rel(ba.grad, gb) < 1e-4
+
+
+CONVT_CASES = [
+    # B, Cin, H, Cout, k, stride, pad
+    (4, 7, 4, 5, 4, 2, 1),
+    (4, 256, 1, 384, 4, 1, 0),
+    (2, 108, 32, 108, 4, 2, 1),
+    (4, 3, 8, 3, 4, 2, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONVT_CASES)
+def test_conv_transpose(ops, case):
+    B, Cin, H, Cout, k, s, p = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Cin, Cout, k, k, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64, requires_grad=True)
+    y = F.conv_transpose2d(x, w, b, stride=s, padding=p)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    gx, gw, gb = torch.autograd.grad(y, (x, w, b), gy)
+    geo = ops.convT_geo(B, Cin, H, H, Cout, k, s, p)
+    xa = cn(x).requires_grad_()
+    wa = w.detach().float().to(DEV).requires_grad_()
+    ba = b.detach().float().to(DEV).requires_grad_()
+    ya = ops.conv2d(xa, wa, ba, geo, 1.0)
+    assert rel(nc(ya), y) < 1e-4
+    ya.backward(cn(gy))
+    assert rel(nc(xa.grad), gx) < 1e-4 and rel(wa.grad, gw) < 1e-4 and rel(ba.grad, gb) < 1e-4
+
+
+@pytest.mark.parametrize("B,cin,cout", [(4, 256, 256), (64, 4100, 4100), (8, 4100, 1), (64, 256, 3072)])
+def test_linear(ops, B, cin, cout):
+    g = torch.Generator().manual_seed(B + cin)
+    x = torch.randn(B, cin, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(cout, generator=g, dtype=torch.float64, requires_grad=True)
+    c = cin ** -0.5
+    y = F.linear(x, w * c, b)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    gx, gw, gb = torch.autograd.grad(y, (x, w, b), gy)
+    xa = x.detach().t().contiguous().float().to(DEV).requires_grad_()
+    wa = w.detach().float().to(DEV).requires_grad_()
+    ba = b.detach().float().to(DEV).requires_grad_()
+    ya = ops.linear(xa, wa, ba, c)
+    assert rel(ya.t(), y) < 1e-4
+    ya.backward(gy.t().contiguous().float().to(DEV))
+    assert rel(xa.grad.t(), gx) < 1e-4 and rel(wa.grad, gw) < 1e-4 and rel(ba.grad, gb) < 1e-4
+
+
+@pytest.mark.parametrize("B,cin,cout,H,k", [(4, 48, 54, 16, 3), (4, 96, 96, 8, 5), (8, 390, 192, 4, 1)])
+def test_modconv(ops, B, cin, cout, H, k):
+    """Batch-shared modulated conv vs the reference's per-sample grouped conv (generator_13_5.py:234-248)."""
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.randn(B, cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    s = torch.randn(B, cin, generator=g, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(cout, cin, k, k, generator=g, dtype=torch.float64, requires_grad=True)
+    c = (cin * k * k) ** -0.5
+    wts = (W * c)[None] * s[:, None, :, None, None]
+    wts = wts * torch.rsqrt(wts.pow(2).sum(dim=(2, 3, 4), keepdim=True) + 1e-8)
+    xp = F.pad(x.reshape(1, -1, H, H), ((k - 1) // 2,) * 4, mode="replicate")
+    y = F.conv2d(xp, wts.reshape(B * cout, cin, k, k), groups=B).reshape(B, cout, H, H)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    gx, gs, gW = torch.autograd.grad(y, (x, s, W), gy)
+    geo = ops.conv_geo(B, cin, H, H, cout, k, 1, (k - 1) // 2)
+    xa = cn(x).requires_grad_()
+    sa = s.detach().t().contiguous().float().to(DEV).requires_grad_()
+    Wa = W.detach().float().to(DEV).requires_grad_()
+    ya = ops.modconv(xa, sa, Wa, geo, c)
+    assert rel(nc(ya), y) < 1e-4
+    ya.backward(cn(gy))
+    assert rel(nc(xa.grad), gx) < 1e-4
+    assert rel(sa.grad.t(), gs) < 1e-4
+    assert rel(Wa.grad, gW) < 1e-4
+
+
+@pytest.mark.parametrize("shape,act", [((5, 4, 8, 8), True), ((300, 64), True), ((3, 64, 64, 64), False),
+                                       ((48, 8, 64, 64), True)])
+def test_bn_act(ops, shape, act):
+    g = torch.Generator().manual_seed(len(shape) + shape[0])
+    C = shape[0]
+    x = (torch.randn(shape, generator=g, dtype=torch.float64) * 3 + 1).requires_grad_()
+    gam = (1 + 0.1 * torch.randn(C, generator=g, dtype=torch.float64)).requires_grad_()
+    bet = (0.1 * torch.randn(C, generator=g, dtype=torch.float64)).requires_grad_()
+    al = (0.25 + 0.05 * torch.randn(C, generator=g, dtype=torch.float64)).requires_grad_()
+    xn = x.transpose(0, 1) if len(shape) == 2 else x.permute(1, 0, 2, 3)   # to reference NC(HW)
+    rm = torch.zeros(C, dtype=torch.float64)
+    rv = torch.ones(C, dtype=torch.float64)
+    y = F.batch_norm(xn, rm, rv, gam, bet, training=True, momentum=0.1, eps=1e-5)
+    if act:
+        y = F.prelu(y, al)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    grads = torch.autograd.grad(y, (x, gam, bet, al) if act else (x, gam, bet), gy)
+    bn = torch.nn.BatchNorm1d(C).to(DEV) if len(shape) == 2 else torch.nn.BatchNorm2d(C).to(DEV)
+    pr = torch.nn.PReLU(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(gam)
+        bn.bias.copy_(bet)
+        pr.weight.copy_(al)
+    xa = x.detach().float().to(DEV).requires_grad_()
+    ya = ops.bn_act(xa, bn, pr if act else None)
+    yref = y.transpose(0, 1) if len(shape) == 2 else y.permute(1, 0, 2, 3)
+    assert rel(ya, yref) < 1e-4
+    assert rel(bn.running_mean, rm) < 1e-5 and rel(bn.running_var, rv) < 1e-5
+    gya = (gy.transpose(0, 1) if len(shape) == 2 else gy.permute(1, 0, 2, 3)).contiguous().float().to(DEV)
+    ya.backward(gya)
+    assert rel(xa.grad, grads[0]) < 1e-4
+    assert rel(bn.weight.grad, grads[1]) < 1e-4 and rel(bn.bias.grad, grads[2]) < 1e-4
+    if act:
+        assert rel(pr.weight.grad, grads[3]) < 1e-4
+
+
+def test_prelu_double_backward(ops):
+    """grad of ||d(sum r*prelu(x))/dx||^2 w.r.t. x, alpha and r -- the GP pattern."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(6, 4, 5, 5, generator=g, dtype=torch.float64, requires_grad=True)
+    a = (0.25 + 0.1 * torch.randn(6, generator=g, dtype=torch.float64)).requires_grad_()
+    r = torch.randn(6, 4, 5, 5, generator=g, dtype=torch.float64, requires_grad=True)
+
+    def run(xx, aa, rr, f):
+        y = f(xx, aa)
+        gxx, = torch.autograd.grad((y * rr).sum(), xx, create_graph=True)
+        ((gxx * gxx).sum() + (gxx * xx).sum()).backward()
+        return xx.grad, aa.grad, rr.grad
+
+    want = run(x, a, r, lambda t, s: F.prelu(t.transpose(0, 1), s).transpose(0, 1))
+    xa = x.detach().float().to(DEV).requires_grad_()
+    aa = a.detach().float().to(DEV).requires_grad_()
+    ra = r.detach().float().to(DEV).requires_grad_()
+    got = run(xa, aa, ra, ops.prelu)
+    for gg, ww in zip(got, want):
+        assert rel(gg, ww) < 1e-5
+
+
+def test_conv_prelu_double_backward(ops):
+    """Double backward through conv -> prelu -> conv (weights and input), as in the critic."""
+    g = torch.Generator().manual_seed(5)
+    B, C, H = 4, 6, 8
+    x = torch.randn(B, 3, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    w1 = torch.randn(C, 3, 3, 3, generator=g, dtype=torch.float64, requires_grad=True)
+    w2 = torch.randn(C, C, 3, 3, generator=g, dtype=torch.float64, requires_grad=True)
+    b1 = torch.randn(C, generator=g, dtype=torch.float64, requires_grad=True)
+    a = (0.25 + 0.1 * torch.randn(C, generator=g, dtype=torch.float64)).requires_grad_()
+
+    def ref(xx, w1, w2, b1, a):
+        y = ref_conv(xx, w1, b1, 3, 1, 1, 1)
+        y = F.prelu(y, a)
+        y = ref_conv(y, w2, None, 3, 2, 1, 1)
+        return y.sum(dim=(1, 2, 3))
+
+    def mine(xx, w1, w2, b1, a):
+        x_c = xx.permute(1, 0, 2, 3).contiguous()
+        y = ops.conv2d(x_c, w1, b1, ops.conv_geo(B, 3, H, H, C, 3, 1, 1), 1.0)
+        y = ops.prelu(y, a)
+        y = ops.conv2d(y, w2, None, ops.conv_geo(B, C, H, H, C, 3, 2, 1), 1.0)
+        return y.sum(dim=(0, 2, 3))
+
+    def gp(f, leaves):
+        out = f(*leaves)
+        gx, = torch.autograd.grad(out.sum(), leaves[0], create_graph=True)
+        loss = ((gx.pow(2).flatten(1).sum(1).sqrt() - 1) ** 2).mean()
+        loss.backward()
+        return [t.grad for t in leaves]
+
+    want = gp(ref, [x, w1, w2, b1, a])
+    got = gp(mine, [t.detach().float().to(DEV).requires_grad_() for t in (x, w1, w2, b1, a)])
+    for gg, ww in zip(got[1:], want[1:]):
+        assert rel(gg, ww) < 1e-4
+    assert rel(got[0], want[0]) < 1e-4
+
+
+@pytest.mark.parametrize("kind,n", [("smooth", 64), ("up2_smooth", 8), ("smooth_down2", 32), ("pool5", 16)])
+def test_resample_and_adjoint(ops, kind, n):
+    from gan_amd import tables
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(3, 5, n, n, generator=g, dtype=torch.float64, requires_grad=True)
+    m = torch.from_numpy(tables.operator_1d(kind, n))
+    y = torch.einsum("oh,pw,bchw->bcop", m, m, x)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    gx, = torch.autograd.grad(y, x, gy)
+    xa = x.detach().float().to(DEV).requires_grad_()
+    ya = ops.resample(xa, kind)
+    assert rel(ya, y) < 1e-5
+    ya.backward(gy.float().to(DEV))
+    assert rel(xa.grad, gx) < 1e-5
+
+
+def test_plane_mean(ops):
+    x = torch.randn(7, 4, 8, 8, dtype=torch.float64)
+    xa = x.float().to(DEV)
+    assert rel(ops.plane_mean(xa), x.mean(dim=(2, 3))) < 1e-6
+
+
+def test_adamw_matches_torch():
+    from gan_amd.optim import FusedAdamW
+    torch.manual_seed(0)
+    m1 = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5)).to(DEV)
+    m2 = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5)).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    o1 = torch.optim.AdamW(m1.parameters(), lr=4e-4, betas=(0.5, 0.999))
+    o2 = FusedAdamW(m2, lr=4e-4, betas=(0.5, 0.999))
+    for it in range(5):
+        x = torch.randn(8, 33, device=DEV)
+        o1.zero_grad()
+        o2.zero_grad()
+        m1(x).pow(2).sum().backward()
+        m2(x).pow(2).sum().backward()
+        o1.step()
+        o2.step()
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        assert torch.allclose(p1, p2, rtol=1e-5, atol=1e-6)
+    assert int(o2.step_count.item()) == 5

@@ -5,22 +5,7 @@ import torch
 
 from oracle import model as om
 from oracle.params import tensor_summary
-from tests._util import fixture, grad_norm_stats, plan, rel_err
-
-# step-level gradient bar (see tests/_util.py:grad_norm_stats for why it is norm-based)
-# D-step: GP double backward; G-step: ~100 sequential BN layers at B=4 (BN1d over 4 samples
-# amplifies rounding where a feature is nearly constant across the batch)
-D_BAR = dict(median=2e-4, p99=2e-3, max=2e-2, vec=1e-3)
-G_BAR = dict(median=2e-4, p99=5e-3, max=1e-1, vec=1e-3)
-
-
-def check_grads(rows, want, bar):
-    med, p99, mx, vec = grad_norm_stats(rows, want)
-    assert med < bar["median"] and p99 < bar["p99"], (med, p99, mx, vec)
-    assert mx < bar["max"] and vec < bar["vec"], (med, p99, mx, vec)
-
-torch.set_num_threads(8)
-
+from tests._util import D_BAR, G_BAR, check_grads, fixture, plan, rel_err
 
 @pytest.fixture(scope="module")
 def P():
