@@ -400,9 +400,22 @@ def modconv(x, s, w, geo, c):
 # ------------------------------------------------------------------------------------------
 
 
+class _SwapNC(Function):
+    """Contiguous [N,C,H,W] <-> [C,N,H,W] swap whose gradient is again contiguous (callers of the
+    reference view input gradients, e.g. ``grad.view(B, -1)`` at wgangp.py:53)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.permute(1, 0, 2, 3).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return _SwapNC.apply(g)
+
+
 def nchw_to_cnhw(x):
-    return x.permute(1, 0, 2, 3).contiguous()
+    return _SwapNC.apply(x)
 
 
 def cnhw_to_nchw(x):
-    return x.permute(1, 0, 2, 3).contiguous()
+    return _SwapNC.apply(x)

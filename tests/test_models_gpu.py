@@ -1,0 +1,127 @@
+"""GPU parity of the drop-in modules and the WGAN-GP steps against the golden fixtures.
+
+Fixtures come from the reference itself (tests/golden/make_golden.py); randomness is replayed
+from the same seeded CPU generator in the reference's draw order (gan_amd.ReplayRNG), so the
+comparison is element for element.  Bars: module outputs 1e-4 norm-relative; step gradients by
+the norm-based bars of tests/_util.py (the same ones the CPU oracle meets)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.params import fill_module, tensor_summary
+from tests._util import fixture, grad_norm_stats, plan, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def P():
+    return plan()
+
+
+@pytest.fixture(scope="module")
+def truth():
+    return fixture("f64_truth.npz")
+
+
+def check_vs_truth(rows, truth_rows, ref_stats):
+    got = grad_norm_stats(rows, truth_rows)
+    bars = [2 * r + 1e-5 for r in ref_stats]
+    assert all(g <= b for g, b in zip(got, bars)), ("gpu-vs-f64", got, "bars", bars)
+    return got
+
+
+@pytest.fixture(scope="module")
+def gan():
+    import gan_amd
+    return gan_amd
+
+
+def make_G(gan, P):
+    G = gan.Generator(256)
+    fill_module(G, P["g_seed"])
+    return G.to(DEV)
+
+
+def make_D(gan, P):
+    D = gan.Discriminator()
+    fill_module(D, P["d_seed"])
+    return D.to(DEV)
+
+
+def test_g_forward_b4(gan, P, truth):
+    fx = fixture("g_fwd_b4.npz")
+    G = make_G(gan, P)
+    rng = gan.ReplayRNG(101, DEV)
+    G.noise_hub.source = rng.noise
+    with torch.no_grad():
+        out = G(torch.from_numpy(fx["z"]).to(DEV))
+    torch.cuda.synchronize()
+    assert tuple(out.shape) == (4, 3, 64, 64)
+    err = rel_err(out.cpu().numpy(), fx["out"])
+    assert err < 1e-3, err
+    assert rel_err(out.cpu().numpy(), truth["g_out"]) < 2 * float(truth["ref_g_out_err"])
+    assert [list(s) for _, s in rng.log] == P["g_noise_shapes_b4"]
+    buf = np.asarray([[float(b.double().sum()), float(b.double().norm())] for _, b in G.named_buffers()])
+    assert rel_err(buf, fx["buffers"]) < 1e-4
+
+
+@pytest.mark.parametrize("B", [4, 8])
+def test_d_forward(gan, P, B):
+    fx = fixture("d_fwd.npz")
+    D = make_D(gan, P)
+    x = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(200 + B)).to(DEV)
+    with torch.no_grad():
+        out = D(x)
+    assert tuple(out.shape) == (B, 1)
+    assert rel_err(out.cpu().numpy(), fx[f"out_b{B}"]) < 1e-5
+
+
+def _rows(mod, names):
+    params = dict(mod.named_parameters())
+    rows = []
+    for n in names:
+        p = params[n]
+        rows.append(tensor_summary(p.grad) if p.grad is not None else [np.nan] * 11)
+    return rows
+
+
+@pytest.mark.parametrize("B,img_seed,rng_seed", [(4, 300, 301), (8, 310, 311)])
+def test_d_step(gan, P, truth, B, img_seed, rng_seed):
+    fx = fixture(f"d_step_b{B}.npz")
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(rng_seed, DEV))
+    images = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed)).to(DEV)
+    names = [n for n, _, _ in P["d_params"]]
+    before = {n: p.detach().clone() for n, p in D.named_parameters()}
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, B)]
+    assert rel_err(losses, fx["losses"]) < 1e-4, (losses, fx["losses"])
+    # draw order: z, 253 noises, eps
+    kinds = [k for k, _ in tr.rng.log]
+    assert kinds[0] == "randn" and kinds[-1] == "rand" and len(kinds) == 2 + len(P["g_noise_shapes_b4"])
+    rows = _rows(D, names)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx["has_grad"]).all()
+    check_vs_truth(rows, truth[f"d{B}_grads"], truth[f"ref_d{B}_stats"])
+    assert rel_err(losses, truth[f"d{B}_losses"]) <= 2 * float(truth[f"ref_d{B}_loss_err"]) + 1e-6
+    params = dict(D.named_parameters())
+    dl = np.asarray([tensor_summary((params[n].detach() - before[n]) / 4e-4)[1] for n in names])
+    assert rel_err(dl, fx["deltas"][:, 1]) < 2e-3
+
+
+def test_g_step(gan, P, truth):
+    fx = fixture("g_step_b4.npz")
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(401, DEV))
+    names = [n for n, _, _ in P["g_params"]]
+    gen, g_loss = tr.generator_trainstep(4)
+    assert rel_err([float(g_loss.detach())], fx["g_loss"]) < 1e-4
+    assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-3
+    rows = _rows(G, names)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx["has_grad"]).all()
+    check_vs_truth(rows, truth["g_grads"], truth["ref_g_stats"])
+    # the critic was frozen only for the backward (its weight gradient is dead work there)
+    assert all(p.requires_grad for n, p in D.named_parameters() if not n.endswith("kernel"))
+    assert float(tr.optimizer_D.flat.grad.abs().sum()) == 0.0
