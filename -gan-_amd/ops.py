@@ -76,7 +76,42 @@ def linear_geo(B, cin, cout):
     return Geo(B, cin, 1, 1, cout, 1, 1, 1, 1, 0, _lib.PAD_ZERO, False)
 
 
+class FlopCounter:
+    """Counts MFMA-GEMM FLOPs issued through the conv wrappers while ``enabled`` (host side;
+    used by bench.py on an eager iteration to report executed vs algorithmic work)."""
+
+    enabled = False
+    flops = 0
+    launches = 0
+    record = None          # optional list receiving (op, geo, has_xscale, has_yscale)
+
+    @classmethod
+    def add(cls, geo: "Geo", op: str = "", xs=False, ys=False):
+        if cls.record is not None:
+            cls.record.append((op, geo, xs, ys))
+        if cls.enabled:
+            cls.flops += 2 * geo.B * geo.OH * geo.OW * geo.Cout * geo.Cin * geo.K * geo.K if not geo.transposed \
+                else 2 * geo.B * geo.H * geo.W * geo.Cout * geo.Cin * geo.K * geo.K
+            cls.launches += 1
+
+
+def _need(t, n, what):
+    """Host-side operand check before any launch: a wrong size must raise, never fault."""
+    if t is not None and t.numel() != n:
+        raise _lib.GanAmdError(f"{what}: expected {n} elements, got {tuple(t.shape)}")
+
+
+def _w_numel(geo):
+    return geo.Cin * geo.Cout * geo.K * geo.K
+
+
 def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0):
+    _need(x, geo.Cin * geo.B * geo.H * geo.W, "conv_fwd x")
+    _need(w, _w_numel(geo), "conv_fwd w")
+    _need(bias, geo.Cout, "conv_fwd bias")
+    _need(xs, geo.Cin * geo.B, "conv_fwd x_scale")
+    _need(ys, geo.Cout * geo.B, "conv_fwd y_scale")
+    FlopCounter.add(geo, "fwd", xs is not None, ys is not None)
     y = torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device, dtype=torch.float32)
     check(LIB.ganamd_conv_fwd(geo.desc(), ptr(x), ptr(w), ptr(bias), ptr(xs), ptr(ys), float(alpha), ptr(y),
                               stream()), "conv_fwd")
@@ -84,6 +119,10 @@ def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0):
 
 
 def _conv_dgrad(geo: Geo, gy, w, gys=None, alpha=1.0):
+    _need(gy, geo.Cout * geo.B * geo.OH * geo.OW, "conv_dgrad gy")
+    _need(w, _w_numel(geo), "conv_dgrad w")
+    _need(gys, geo.Cout * geo.B, "conv_dgrad gy_scale")
+    FlopCounter.add(geo, "dgrad", gys is not None, False)
     gx = torch.empty((geo.Cin, geo.B, geo.H, geo.W), device=gy.device, dtype=torch.float32)
     nb = geo.ws_bytes(_lib.CONV_DGRAD)
     ws = workspace(nb, gy.device) if nb else None
@@ -93,6 +132,12 @@ def _conv_dgrad(geo: Geo, gy, w, gys=None, alpha=1.0):
 
 
 def _conv_wgrad(geo: Geo, x, gy, xs=None, gys=None, alpha=1.0, out=None, accumulate=False):
+    _need(x, geo.Cin * geo.B * geo.H * geo.W, "conv_wgrad x")
+    _need(gy, geo.Cout * geo.B * geo.OH * geo.OW, "conv_wgrad gy")
+    _need(xs, geo.Cin * geo.B, "conv_wgrad x_scale")
+    _need(gys, geo.Cout * geo.B, "conv_wgrad gy_scale")
+    _need(out, _w_numel(geo), "conv_wgrad out")
+    FlopCounter.add(geo, "wgrad", xs is not None, gys is not None)
     shape = (geo.Cin, geo.Cout, geo.K, geo.K) if geo.transposed else (geo.Cout, geo.Cin, geo.K, geo.K)
     gw = out if out is not None else torch.empty(shape, device=x.device, dtype=torch.float32)
     check(LIB.ganamd_conv_wgrad(geo.desc(), ptr(x), ptr(gy), ptr(xs), ptr(gys), float(alpha), ptr(gw),
@@ -189,6 +234,7 @@ class PReLU(Function):
     def forward(ctx, x, a):
         x = _c(x)
         C, L = _rows(x)
+        _need(a, C, "prelu alpha")
         y = torch.empty_like(x)
         check(LIB.ganamd_prelu_fwd(ptr(x), ptr(a), C, L, ptr(y), stream()), "prelu_fwd")
         ctx.save_for_backward(x, a)
@@ -246,6 +292,9 @@ class BNAct(Function):
     def forward(ctx, x, gamma, beta, alpha, running_mean, running_var, momentum, eps):
         x = _c(x)
         C, L = _rows(x)
+        for t, nm in ((gamma, "gamma"), (beta, "beta"), (alpha, "alpha"), (running_mean, "running_mean"),
+                      (running_var, "running_var")):
+            _need(t, C, f"bn_act {nm}")
         y = torch.empty_like(x)
         mean = torch.empty(C, device=x.device, dtype=torch.float32)
         invstd = torch.empty_like(mean)
@@ -287,6 +336,8 @@ def bn_act(x, bn: torch.nn.modules.batchnorm._BatchNorm, act: torch.nn.PReLU | N
 def _resample(x, n_in, n_out, tab):
     idx, w, k = tab
     C, B = x.shape[0], x.shape[1]
+    if x.dim() != 4 or x.shape[2] != n_in or x.shape[3] != n_in or idx.shape[0] != n_out:
+        raise _lib.GanAmdError(f"resample: input {tuple(x.shape)} vs table {n_in}->{n_out}")
     y = torch.empty((C, B, n_out, n_out), device=x.device, dtype=torch.float32)
     check(LIB.ganamd_resample2d(ptr(x), C * B, n_in, n_in, ptr(y), n_out, n_out, iptr(idx), ptr(w), k, iptr(idx),
                                 ptr(w), k, stream()), "resample2d")

@@ -1,0 +1,194 @@
+"""WGAN-GP throughput benchmark: G13_5 + D9_4, 64x64x3, n_critic = 5, fp32, on 1..8 MI355X.
+
+One timed "step" is one WGAN-GP iteration = 5 critic steps (each: no-grad G forward, critic on a
+fresh real batch and on the fake batch, gradient penalty with its double backward, AdamW) + 1
+generator step (G forward, critic forward/backward into G, AdamW), exactly train/wgangp.py:20-71
+with the iteration structure of the metric in BASELINE.json.  Per GPU the batch is 64 (config 2);
+with N ranks (torchrun) every rank runs its own 64-image shard and the gradients of each optimizer
+step are all-reduced over RCCL (config 3 at N = 8: 512 images).
+
+value = images per second over all ranks = 64 * N * steps / max-over-ranks(timed seconds).
+The real batches are synthetic N(0,1) [64,3,64,64] tensors drawn on the device inside the step
+(the reference's ImageNet-normalised data has that scale); weights are the reference's init
+distributions (random, seeded).
+
+Also reported (rank 0):
+  roofline      algorithmic conv FLOPs per iteration (1,559.5 GFLOP per image)
+                over the measured iteration time, against the fp32 MFMA peak (157.3 TFLOP/s);
+                plus the conv-GEMM FLOPs this build actually issues per iteration.
+  cpu_baseline  the CPU oracle (oracle/model.py, fp32 PyTorch-CPU restatement pinned to the
+                reference's golden fixtures) timed on the host: 1 D-step + 1 G-step at B=4.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "images/sec per WGAN-GP iter (G13_5+D9_4, 64x64, n_critic=5) at 1/2/4/8 MI355X"
+ALGO_GFLOP_PER_IMAGE = 1559.5
+FP32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md, chip-level parameters
+N_CRITIC = 5
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU")
+    ap.add_argument("--mode", choices=["eager", "graph"], default="eager")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def setup_dist(n):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    assert world == n or world == 1, f"--gpus {n} but WORLD_SIZE {world}"
+    return world, rank, local
+
+
+def cpu_baseline(threads):
+    """Time the CPU oracle: 1 D-step + 1 G-step at B=4 -> images/sec of a full iteration."""
+    from oracle import model as om
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    GP, DP = om.Params(lazy=True, generator=g), om.Params(lazy=True, generator=g)
+    draw = om.Draw(1)
+    with torch.no_grad():  # materialise every parameter once (lazy init) outside the timing
+        om.generator(GP, torch.randn(4, 256, 1, 1), draw.randn)
+        om.discriminator(DP, torch.randn(4, 3, 64, 64))
+    tr = om.WGANGP(GP, DP)
+    B = 4
+    imgs = torch.randn(B, 3, 64, 64, generator=g)
+    t0 = time.perf_counter()
+    tr.discriminator_trainstep(imgs, B, draw)
+    t1 = time.perf_counter()
+    tr.generator_trainstep(B, draw)
+    t2 = time.perf_counter()
+    t_iter = N_CRITIC * (t1 - t0) + (t2 - t1)
+    return {"value": B / t_iter, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"CPU oracle (fp32 PyTorch-CPU restatement), B=4: 1 D-step {t1 - t0:.2f}s + 1 G-step "
+                      f"{t2 - t1:.2f}s, t_iter = 5*t_D + t_G = {t_iter:.1f}s; nproc={os.cpu_count()}"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args.gpus)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    import gan_amd
+    from gan_amd import ops
+    from gan_amd.dist import attach_grad_sync
+
+    torch.manual_seed(1234)                         # identical initial weights on every rank
+    G = gan_amd.Generator(256).to(dev)
+    D = gan_amd.Discriminator().to(dev)
+    torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
+    tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev))
+    if world > 1:
+        attach_grad_sync(tr.optimizer_G)
+        attach_grad_sync(tr.optimizer_D)
+    B = args.batch
+
+    def iteration():
+        for _ in range(N_CRITIC):
+            images = torch.randn(B, 3, 64, 64, device=dev)
+            tr.discriminator_trainstep(images, B)
+        tr.generator_trainstep(B)
+
+    # warm-up (eager); the first one also counts the conv FLOPs this build issues
+    ops.FlopCounter.enabled = True
+    iteration()
+    ops.FlopCounter.enabled = False
+    issued_flops = ops.FlopCounter.flops
+    for _ in range(max(0, args.warmup - 1)):
+        iteration()
+    torch.cuda.synchronize()
+
+    step = iteration
+    if args.mode == "graph":
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            iteration()
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(graph):
+            iteration()
+        torch.cuda.synchronize()
+        step = graph.replay
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    wall0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - wall0
+    if world > 1:
+        dist.barrier()
+    secs = ev0.elapsed_time(ev1) / 1e3
+    t = torch.tensor([secs], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    secs = float(t)
+
+    if rank == 0:
+        print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
+              f"issued GEMM launches/iter {ops.FlopCounter.launches}", file=sys.stderr, flush=True)
+        n_img = B * world * args.steps
+        t_iter = secs / args.steps
+        achieved = ALGO_GFLOP_PER_IMAGE * 1e9 * B / t_iter / 1e12      # per GPU
+        out = {
+            "metric": METRIC,
+            "value": n_img / secs,
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * t_iter,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic N(0,1) real batches drawn on device each critic step; random reference-init weights",
+            "config": {"workload": "G13_5+D9_4 WGAN-GP iteration (5 critic steps with GP + 1 generator step), "
+                                   "64x64x3", "global_batch": B * world, "per_gpu_batch": B, "n_critic": N_CRITIC,
+                       "parallelism": f"dp{world}", "mode": args.mode},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "conv_gemm/wgrad_gemm implicit-GEMM family (99% of algorithmic FLOPs)",
+                         "algorithmic_gflop_per_iter": ALGO_GFLOP_PER_IMAGE * B,
+                         "issued_gemm_gflop_per_iter": issued_flops / 1e9},
+            "wall_s": wall,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
