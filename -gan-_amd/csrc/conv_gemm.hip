@@ -16,11 +16,15 @@
 // discriminator_9_4.py:38-40), the grouped per-sample conv (generator_13_5.py:243-247),
 // nn.ConvTranspose2d (generator_13_5.py:156,594), and their autograd backward.
 //
-// Tiling: 256 threads = 4 waves; block tile BM x BN, K-step BK; each wave owns a
-// (32*TM) x (32*TN) sub-tile built from v_mfma_f32_32x32x2f32.  LDS holds both operand tiles
-// k-major ([k][m], [k][n]) so a lane's A/B fragment element is one conflict-free ds_read_b32;
-// tiles are double buffered (one barrier per K-step) and the next tile's global gather is
-// issued into registers before the MFMAs of the current one.
+// Tiling.  256 threads = 4 waves; block tile BM x BN, K-step BK = 16; each wave owns a
+// (32*TM) x (32*TN) sub-tile of v_mfma_f32_32x32x2f32.  Both operand tiles sit in LDS
+// "k-contiguous" ([m][k], [n][k], row stride BK+2 floats) so that one lane reads its 8 k-values
+// of a row with four conflict-free ds_read_b64.  The MFMA k index is permuted: in step s lane
+// half h contributes k = 8h + s, identically for A and B, so the product is unchanged.
+// Global gathers are branch-free (every lane loads from a valid address, padding is a select)
+// so hipcc keeps all of a tile's loads in flight; per-(channel,sample) scales are applied when
+// the prefetched registers are written to LDS.  Tiles are double buffered (one barrier per
+// K-step) and the next tile's gather is issued before the current tile's MFMAs.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,10 +34,30 @@
 #include "../../include/ganamd.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int BK = 16;
+constexpr int LDK = BK + 2;  // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
+
+enum GatherMode { kZero = 0, kReplicate = 1, kTransposed = 2 };
+
+// Buffer loads: a 32-bit byte offset against a range-checked descriptor.  An offset past the
+// end returns 0 in hardware, so padding / tails are a select of the OFFSET, never a branch
+// around the load (hipcc would otherwise branch and wait vmcnt per element).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kOOB = (int)0x80000000;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float bload(rsrc_t r, int byte_off) {
+  asm("" : "+v"(byte_off));  // opaque: keeps hipcc from re-splitting the select into branches
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
 
 // Gather of a CNHW source tensor as a GEMM operand indexed by (tap, channel, n).
 struct Gather {
@@ -42,13 +66,16 @@ struct Gather {
   int C, B, H, W;      // source extents
   int OH, OW;          // GEMM spatial extents (n = (b, oh, ow))
   int KW, stride, pad;
-  int mode;            // 0: conv, zero pad; 1: conv, replication pad; 2: transposed conv
+  int mode;
+
+  __device__ int src_bytes() const { return 4 * C * B * H * W; }
+  __device__ int scale_bytes() const { return 4 * C * B; }
 };
 
-// Offset of source pixel feeding output (oh, ow) through tap (kh, kw), or -1 if it is padding.
+// Offset of the source pixel feeding output (oh, ow) through tap (kh, kw), or -1 for padding.
+template <int MODE>
 __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int kh, int kw) {
-  int ih, iw;
-  if (g.mode == 2) {
+  if (MODE == kTransposed) {
     int th = oh + g.pad - kh, tw = ow + g.pad - kw;
     if (th < 0 || tw < 0) return -1;
     if (g.stride > 1) {
@@ -57,24 +84,22 @@ __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int k
       tw /= g.stride;
     }
     if (th >= g.H || tw >= g.W) return -1;
-    ih = th;
-    iw = tw;
-  } else {
-    ih = oh * g.stride - g.pad + kh;
-    iw = ow * g.stride - g.pad + kw;
-    if (g.mode == 1) {
-      ih = min(max(ih, 0), g.H - 1);
-      iw = min(max(iw, 0), g.W - 1);
-    } else if (ih < 0 || iw < 0 || ih >= g.H || iw >= g.W) {
-      return -1;
-    }
+    return th * g.W + tw;
   }
+  int ih = oh * g.stride - g.pad + kh;
+  int iw = ow * g.stride - g.pad + kw;
+  if (MODE == kReplicate) {
+    ih = min(max(ih, 0), g.H - 1);
+    iw = min(max(iw, 0), g.W - 1);
+    return ih * g.W + iw;
+  }
+  if (ih < 0 || iw < 0 || ih >= g.H || iw >= g.W) return -1;
   return ih * g.W + iw;
 }
 
 struct ConvArgs {
   const float* w;      // A(m, t, c) = w[m*sm + c*sc + t*st]
-  long sm, sc, st;
+  int sm, sc, st, w_bytes;
   int M, Ck, T;        // GEMM rows, channels per tap, taps
   Gather g;
   float* y;            // Y[m][n]
@@ -88,57 +113,73 @@ struct ConvArgs {
 struct WgradArgs {
   const float* a;      // A(m, n) = a[m*lda + n] (* ascale[m][b])
   const float* ascale;
-  long lda;
+  int lda, a_bytes;
   int M, J, K, ohw;    // rows, gathered channels, K = B*OH*OW
   Gather g;            // B(n, j): channel j of the gather at tap t
   float* out;          // out[m*om + j*oj + t*ot]
-  long om, oj, ot;
+  int om, oj, ot;
   float alpha;
   int kt_per_split, splits, atomic;
 };
 
-template <int BM, int BN, int BK, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN>
 struct TileCfg {
   static constexpr int TM = BM / (32 * WGM);
   static constexpr int TN = BN / (32 * WGN);
-  static constexpr int PA = BM + 2;  // +2 floats: the k-strided LDS stores hit distinct banks
-  static constexpr int PB = BN + 2;
   static_assert(WGM * WGN == 4, "4 waves per block");
   static_assert(TM * 32 * WGM == BM && TN * 32 * WGN == BN, "tile must split into 32x32 MFMAs");
-  static_assert(kThreads % BK == 0, "k index must be thread-invariant");
 };
 
-// One K-step of MFMAs from LDS.  lane l supplies A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31].
-template <class C, int BK>
-__device__ __forceinline__ void mfma_step(const float* __restrict__ As, const float* __restrict__ Bs,
+// Read this lane's 8 k-values of one 32-row fragment: rows r of the [row][k] tile, k = 8h..8h+7.
+__device__ __forceinline__ void read_frag(const float* __restrict__ base, float (&v)[8]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 t = *reinterpret_cast<const f32x2*>(base + 2 * q);
+    v[2 * q] = t[0];
+    v[2 * q + 1] = t[1];
+  }
+}
+
+// One BK=16 K-step of MFMAs for a wave.  In step s lane half h supplies k = 8h + s.
+template <class C>
+__device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
                                           f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn) {
   const int r = lane & 31, h = lane >> 5;
+  float a[C::TM][8], b[C::TN][8];
 #pragma unroll
-  for (int s = 0; s < BK / 2; ++s) {
-    const int kk = 2 * s + h;
-    float a[C::TM], b[C::TN];
+  for (int i = 0; i < C::TM; ++i) read_frag(As + ((wm * C::TM + i) * 32 + r) * LDK + 8 * h, a[i]);
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i) a[i] = As[kk * C::PA + (wm * C::TM + i) * 32 + r];
+  for (int j = 0; j < C::TN; ++j) read_frag(Bs + ((wn * C::TN + j) * 32 + r) * LDK + 8 * h, b[j]);
 #pragma unroll
-    for (int j = 0; j < C::TN; ++j) b[j] = Bs[kk * C::PB + (wn * C::TN + j) * 32 + r];
+  for (int s = 0; s < 8; ++s)
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-  }
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+}
+
+template <class C>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 }
 
 // ------------------------------------------------------------------------------------------
 // forward / dgrad / transposed: K = (tap, channel), N = output pixels
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
 __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
-  using C = TileCfg<BM, BN, BK, WGM, WGN>;
+  using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int EA = BK * BM / kThreads;
   constexpr int EB = BK * BN / kThreads;
-  static_assert(kThreads % BN == 0 || BN % kThreads == 0, "B mapping");
-  __shared__ float As[2][BK * C::PA];
-  __shared__ float Bs[2][BK * C::PB];
+  static_assert(kThreads % BN == 0, "B mapping: n fixed per thread");
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -149,13 +190,10 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
   const int kt1 = min(kt_total, kt0 + p.kt_per_split);
   if (kt0 >= kt1) return;
 
-  // A mapping: k fixed per thread, m strided
-  const int a_k = tid % BK;
-  const int a_m = tid / BK;
+  // A mapping: k fixed per thread, m strided.  B mapping: n fixed per thread, k strided.
+  const int a_k = tid % BK, a_m = tid / BK;
   constexpr int A_MSTEP = kThreads / BK;
-  // B mapping: n fixed per thread, k strided
-  const int b_n = tid % BN;
-  const int b_k = tid / BN;
+  const int b_n = tid % BN, b_k = tid / BN;
   constexpr int B_KSTEP = kThreads / BN;
 
   const Gather& g = p.g;
@@ -168,10 +206,13 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     oh = rr / g.OW;
     ow = rr - oh * g.OW;
   }
-  const long cstride = (long)g.B * g.H * g.W;
-  const float* src_b = g.src + (long)bb * g.H * g.W;
+  const int cstride = g.B * g.H * g.W;
+  const int img = bb * g.H * g.W;
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
 
-  float ra[EA], rb[EB];
+  float ra[EA], rb[EB], rs[EB];
   int cur_t = -1, sp = -1;
 
   auto gload = [&](int kt) {
@@ -179,43 +220,34 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     const int c0 = (kt - t * nct) * BK;
     if (t != cur_t) {
       cur_t = t;
-      sp = n_ok ? tap_offset(g, oh, ow, t / g.KW, t - (t / g.KW) * g.KW) : -1;
+      const int kh = t / g.KW;
+      sp = n_ok ? tap_offset<MODE>(g, oh, ow, kh, t - kh * g.KW) : -1;
     }
-    {
-      const int c = c0 + a_k;
-      const bool cok = c < p.Ck;
-      const float* wp = p.w + (long)c * p.sc + (long)t * p.st;
+    const int ca = c0 + a_k;
+    const bool caok = ca < p.Ck;
+    const int abase = ca * p.sc + t * p.st;
 #pragma unroll
-      for (int e = 0; e < EA; ++e) {
-        const int m = m0 + a_m + e * A_MSTEP;
-        ra[e] = (cok && m < p.M) ? wp[(long)m * p.sm] : 0.f;
-      }
+    for (int e = 0; e < EA; ++e) {
+      const int m = m0 + a_m + e * A_MSTEP;
+      ra[e] = bload(rw, (caok && m < p.M) ? 4 * (abase + m * p.sm) : kOOB);
     }
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
       const int c = c0 + b_k + e * B_KSTEP;
-      float v = 0.f;
-      if (sp >= 0 && c < p.Ck) {
-        v = src_b[(long)c * cstride + sp];
-        if (g.scale) v *= g.scale[(long)c * g.B + bb];
-      }
-      rb[e] = v;
+      const bool ok = sp >= 0 && c < p.Ck;
+      rb[e] = bload(rx, ok ? 4 * (img + c * cstride + sp) : kOOB);
+      if (BSCALE) rs[e] = bload(rsc, ok ? 4 * (c * g.B + bb) : kOOB);
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][a_k * C::PA + a_m + e * A_MSTEP] = ra[e];
+    for (int e = 0; e < EA; ++e) As[buf][(a_m + e * A_MSTEP) * LDK + a_k] = ra[e];
 #pragma unroll
-    for (int e = 0; e < EB; ++e) Bs[buf][(b_k + e * B_KSTEP) * C::PB + b_n] = rb[e];
+    for (int e = 0; e < EB; ++e) Bs[buf][b_n * LDK + b_k + e * B_KSTEP] = BSCALE ? rb[e] * rs[e] : rb[e];
   };
 
   f32x16 acc[C::TM][C::TN];
-#pragma unroll
-  for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  zero_acc<C>(acc);
 
   gload(kt0);
   sstore(0);
@@ -224,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_step<C, BK>(As[buf], Bs[buf], acc, lane, wm, wn);
+    mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -243,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
         float v = p.alpha * acc[i][j][r];
-        if (p.oscale) v *= p.oscale[(long)m * g.B + b];
+        if (p.oscale) v *= p.oscale[m * g.B + b];
         if (add_bias) v += p.bias[m];
         float* dst = p.y + (long)m * p.N + n;
         if (p.atomic)
@@ -258,14 +290,14 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 // ------------------------------------------------------------------------------------------
 // wgrad: K = output pixels n, M = output channels of the conv, N = gathered channels at tap t
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
 __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
-  using C = TileCfg<BM, BN, BK, WGM, WGN>;
+  using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int EA = BK * BM / kThreads;
   constexpr int EB = BK * BN / kThreads;
-  constexpr int MSTEP = kThreads / BK;
-  __shared__ float As[2][BK * C::PA];
-  __shared__ float Bs[2][BK * C::PB];
+  constexpr int RSTEP = kThreads / BK;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -279,11 +311,16 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
 
   const Gather& g = p.g;
   const int kh = t / g.KW, kw = t - kh * g.KW;
-  const long cstride = (long)g.B * g.H * g.W;
-  const int tk = tid % BK;   // k fixed per thread for both operands
+  const int cstride = g.B * g.H * g.W;
+  const int tk = tid % BK;   // k (pixel) fixed per thread for both operands
   const int tr = tid / BK;   // row (m or j) base
 
-  float ra[EA], rb[EB];
+  const rsrc_t ra_r = make_rsrc(p.a, p.a_bytes);
+  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t rsa_r = make_rsrc(SCALED ? p.ascale : p.a, SCALED ? 4 * p.M * g.B : 0);
+  const rsrc_t rsb_r = make_rsrc(SCALED ? g.scale : g.src, SCALED ? g.scale_bytes() : 0);
+
+  float ra[EA], rb[EB], rsa[EA], rsb[EB];
   auto gload = [&](int kt) {
     const int n = kt * BK + tk;
     const bool nok = n < p.K;
@@ -292,44 +329,33 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
       b = n / p.ohw;
       const int rr = n - b * p.ohw;
       const int oh = rr / g.OW;
-      sp = tap_offset(g, oh, rr - oh * g.OW, kh, kw);
+      sp = tap_offset<MODE>(g, oh, rr - oh * g.OW, kh, kw);
     }
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
-      const int m = m0 + tr + e * MSTEP;
-      float v = 0.f;
-      if (nok && m < p.M) {
-        v = p.a[(long)m * p.lda + n];
-        if (p.ascale) v *= p.ascale[(long)m * g.B + b];
-      }
-      ra[e] = v;
+      const int m = m0 + tr + e * RSTEP;
+      const bool ok = nok && m < p.M;
+      ra[e] = bload(ra_r, ok ? 4 * (m * p.lda + n) : kOOB);
+      if (SCALED) rsa[e] = bload(rsa_r, ok ? 4 * (m * g.B + b) : kOOB);
     }
-    const float* src_b = g.src + (long)b * g.H * g.W + sp;
+    const int img = b * g.H * g.W;
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
-      const int jj = j0 + tr + e * MSTEP;
-      float v = 0.f;
-      if (sp >= 0 && jj < p.J) {
-        v = src_b[(long)jj * cstride];
-        if (g.scale) v *= g.scale[(long)jj * g.B + b];
-      }
-      rb[e] = v;
+      const int jj = j0 + tr + e * RSTEP;
+      const bool ok = sp >= 0 && jj < p.J;
+      rb[e] = bload(rx, ok ? 4 * (img + jj * cstride + sp) : kOOB);
+      if (SCALED) rsb[e] = bload(rsb_r, ok ? 4 * (jj * g.B + b) : kOOB);
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][tk * C::PA + tr + e * MSTEP] = ra[e];
+    for (int e = 0; e < EA; ++e) As[buf][(tr + e * RSTEP) * LDK + tk] = SCALED ? ra[e] * rsa[e] : ra[e];
 #pragma unroll
-    for (int e = 0; e < EB; ++e) Bs[buf][tk * C::PB + tr + e * MSTEP] = rb[e];
+    for (int e = 0; e < EB; ++e) Bs[buf][(tr + e * RSTEP) * LDK + tk] = SCALED ? rb[e] * rsb[e] : rb[e];
   };
 
   f32x16 acc[C::TM][C::TN];
-#pragma unroll
-  for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  zero_acc<C>(acc);
 
   gload(kt0);
   sstore(0);
@@ -338,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_step<C, BK>(As[buf], Bs[buf], acc, lane, wm, wn);
+    mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -353,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
-        float* dst = p.out + (long)m * p.om + (long)jj * p.oj + (long)t * p.ot;
+        float* dst = p.out + m * p.om + jj * p.oj + t * p.ot;
         const float v = p.alpha * acc[i][j][r];
         if (p.atomic)
           atomicAdd(dst, v);
@@ -391,7 +417,7 @@ __global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict_
 // ------------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
 hipError_t launch_conv(ConvArgs p, hipStream_t st) {
   const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
   const int nct = (p.Ck + BK - 1) / BK;
@@ -409,37 +435,60 @@ hipError_t launch_conv(ConvArgs p, hipStream_t st) {
     hipError_t e = hipMemsetAsync(p.y, 0, sizeof(float) * (size_t)p.M * p.N, st);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WGM, WGN>), dim3(gx, gy, splits), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3(gx, gy, splits), dim3(kThreads), 0,
+                     st, p);
   return hipGetLastError();
 }
 
-hipError_t dispatch_conv(const ConvArgs& p, hipStream_t st) {
-  if (p.M <= 32) return launch_conv<32, 256, 16, 1, 4>(p, st);
-  if (p.M <= 64) return launch_conv<64, 128, 16, 2, 2>(p, st);
-  if (p.M <= 96) return launch_conv<96, 128, 16, 1, 4>(p, st);
-  return launch_conv<128, 128, 16, 2, 2>(p, st);
+template <int MODE, bool BSCALE>
+hipError_t dispatch_conv_tile(const ConvArgs& p, hipStream_t st) {
+  if (p.M <= 32) return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, st);
+  if (p.M <= 64) return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, st);
+  if (p.M <= 96) return launch_conv<96, 128, 1, 4, MODE, BSCALE>(p, st);
+  return launch_conv<128, 128, 2, 2, MODE, BSCALE>(p, st);
 }
 
-template <int BM, int BN, int BK, int WGM, int WGN>
-hipError_t launch_wgrad(WgradArgs p, int T, int accumulate, hipStream_t st) {
+hipError_t dispatch_conv(const ConvArgs& p, hipStream_t st) {
+  const bool s = p.g.scale != nullptr;
+  switch (p.g.mode) {
+    case kZero: return s ? dispatch_conv_tile<kZero, true>(p, st) : dispatch_conv_tile<kZero, false>(p, st);
+    case kReplicate:
+      return s ? dispatch_conv_tile<kReplicate, true>(p, st) : dispatch_conv_tile<kReplicate, false>(p, st);
+    default:
+      return s ? dispatch_conv_tile<kTransposed, true>(p, st) : dispatch_conv_tile<kTransposed, false>(p, st);
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
+hipError_t launch_wgrad(WgradArgs p, int T, hipStream_t st) {
   const int gx = (p.J + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
   const int kt_total = (p.K + BK - 1) / BK;
   const int blocks = gx * gy * T;
   int splits = 1;
-  if (blocks < 1024) splits = min((1024 + blocks - 1) / blocks, max(1, kt_total / 4));
+  if (blocks < 1024) splits = min((1024 + blocks - 1) / blocks, max(1, kt_total / 8));
   p.kt_per_split = (kt_total + splits - 1) / splits;
   splits = (kt_total + p.kt_per_split - 1) / p.kt_per_split;
   p.splits = splits;
-  p.atomic = splits > 1 || accumulate;
-  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, BK, WGM, WGN>), dim3(gx, gy, T * splits), dim3(kThreads), 0, st, p);
+  p.atomic = 1;
+  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED>), dim3(gx, gy, T * splits), dim3(kThreads), 0,
+                     st, p);
   return hipGetLastError();
 }
 
-hipError_t dispatch_wgrad(const WgradArgs& p, int T, int accumulate, hipStream_t st) {
-  if (p.M <= 32) return launch_wgrad<32, 128, 32, 1, 4>(p, T, accumulate, st);
-  if (p.M <= 64) return launch_wgrad<64, 64, 32, 2, 2>(p, T, accumulate, st);
-  if (p.M <= 96) return launch_wgrad<96, 128, 32, 1, 4>(p, T, accumulate, st);
-  return launch_wgrad<128, 128, 32, 2, 2>(p, T, accumulate, st);
+template <int MODE, bool SCALED>
+hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, hipStream_t st) {
+  if (p.M <= 32) return launch_wgrad<32, 128, 1, 4, MODE, SCALED>(p, T, st);
+  if (p.M <= 64) return launch_wgrad<64, 128, 2, 2, MODE, SCALED>(p, T, st);
+  if (p.M <= 96) return launch_wgrad<96, 128, 1, 4, MODE, SCALED>(p, T, st);
+  return launch_wgrad<128, 128, 2, 2, MODE, SCALED>(p, T, st);
+}
+
+hipError_t dispatch_wgrad(const WgradArgs& p, int T, hipStream_t st) {
+  const bool s = p.ascale != nullptr || p.g.scale != nullptr;
+  if (s && !(p.ascale && p.g.scale)) return hipErrorInvalidValue;  // both scales or none
+  if (p.g.mode == kReplicate)
+    return s ? dispatch_wgrad_tile<kReplicate, true>(p, T, st) : dispatch_wgrad_tile<kReplicate, false>(p, T, st);
+  return s ? dispatch_wgrad_tile<kZero, true>(p, T, st) : dispatch_wgrad_tile<kZero, false>(p, T, st);
 }
 
 bool desc_ok(const ganamd_conv_desc* d) {
@@ -469,17 +518,18 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
   p.w = w;
   if (d->transposed) {  // weights [Cin][Cout][KH][KW]
     p.sm = T;
-    p.sc = (long)d->Cout * T;
+    p.sc = d->Cout * T;
   } else {              // weights [Cout][Cin][KH][KW]
-    p.sm = (long)d->Cin * T;
+    p.sm = d->Cin * T;
     p.sc = T;
   }
   p.st = 1;
+  p.w_bytes = 4 * d->Cin * d->Cout * T;
   p.M = d->Cout;
   p.Ck = d->Cin;
   p.T = T;
   p.g = Gather{x, x_scale, d->Cin, d->B, d->H, d->W, d->OH, d->OW, d->KW, d->stride, d->pad,
-               d->transposed ? 2 : (d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0)};
+               d->transposed ? kTransposed : (d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero)};
   p.y = y;
   p.bias = bias;
   p.oscale = y_scale;
@@ -496,6 +546,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   ConvArgs p{};
   p.w = w;
   p.st = 1;
+  p.w_bytes = 4 * d->Cin * d->Cout * T;
   p.M = d->Cin;
   p.Ck = d->Cout;
   p.T = T;
@@ -504,9 +555,9 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   p.alpha = alpha;
   if (d->transposed) {
     // dX of ConvT = plain zero-padded conv of gy with W viewed [Cin][Cout][KH][KW]
-    p.sm = (long)d->Cout * T;
+    p.sm = d->Cout * T;
     p.sc = T;
-    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, 0};
+    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, kZero};
     p.y = gx;
     p.N = d->B * d->H * d->W;
     p.ohw = d->H * d->W;
@@ -514,11 +565,11 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   }
   // dX of conv = transposed gather of gy into the padded input frame, then fold the pad
   p.sm = T;
-  p.sc = (long)d->Cin * T;
+  p.sc = d->Cin * T;
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
   float* out = d->pad > 0 ? static_cast<float*>(workspace) : gx;
   if (d->pad > 0 && !workspace) return GANAMD_EINVAL;
-  p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, 2};
+  p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
   p.y = out;
   p.N = d->B * Hp * Wp;
   p.ohw = Hp * Wp;
@@ -537,6 +588,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
 int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
                       const float* gy_scale, float alpha, float* gw, int accumulate, hipStream_t stream) {
   if (!desc_ok(d) || !x || !gy || !gw) return GANAMD_EINVAL;
+  if ((x_scale == nullptr) != (gy_scale == nullptr)) return GANAMD_EINVAL;
   const int T = d->KH * d->KW;
   WgradArgs p{};
   p.alpha = alpha;
@@ -545,26 +597,28 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
     // dW[ci][co][t] = sum_n x[ci][n] * gy[co][conv-gather_t(n)]
     p.a = x;
     p.ascale = x_scale;
-    p.lda = (long)d->B * d->H * d->W;
+    p.lda = d->B * d->H * d->W;
+    p.a_bytes = 4 * d->Cin * p.lda;
     p.M = d->Cin;
     p.J = d->Cout;
     p.K = d->B * d->H * d->W;
     p.ohw = d->H * d->W;
-    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, 0};
-    p.om = (long)d->Cout * T;
+    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, kZero};
+    p.om = d->Cout * T;
     p.oj = T;
   } else {
     // dW[co][ci][t] = sum_n gy[co][n] * x[ci][gather_t(n)]
     p.a = gy;
     p.ascale = gy_scale;
-    p.lda = (long)d->B * d->OH * d->OW;
+    p.lda = d->B * d->OH * d->OW;
+    p.a_bytes = 4 * d->Cout * p.lda;
     p.M = d->Cout;
     p.J = d->Cin;
     p.K = d->B * d->OH * d->OW;
     p.ohw = d->OH * d->OW;
     p.g = Gather{x, x_scale, d->Cin, d->B, d->H, d->W, d->OH, d->OW, d->KW, d->stride, d->pad,
-                 d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0};
-    p.om = (long)d->Cin * T;
+                 d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero};
+    p.om = d->Cin * T;
     p.oj = T;
   }
   p.out = gw;
@@ -572,7 +626,7 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
   if (!accumulate) {
     if (hipMemsetAsync(gw, 0, wsz, stream) != hipSuccess) return GANAMD_ELAUNCH;
   }
-  return dispatch_wgrad(p, T, 1, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  return dispatch_wgrad(p, T, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 }  // extern "C"
