@@ -34,9 +34,9 @@ class ConvDesc(ctypes.Structure):
 _SIGS = {
     "ganamd_version": (ctypes.c_char_p, []),
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
-    "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp]),
+    "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),
-    "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp]),
+    "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
     "ganamd_rowreduce_workspace": (c_size_t, [c_int, c_long]),
     "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, vp]),
     "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),

@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "../../include/ganamd.h"
@@ -39,8 +41,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int BK = 16;
-constexpr int LDK = BK + 2;  // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
+constexpr int BK = 16;        // conv K-step (taps x channels)
+constexpr int LDK = BK + 2;   // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
+constexpr int BKW = 32;       // wgrad K-step (pixels): a half-wave reads one full 128-byte line
+constexpr int LDKW = BKW + 2;
 
 enum GatherMode { kZero = 0, kReplicate = 1, kTransposed = 2 };
 
@@ -107,7 +111,8 @@ struct ConvArgs {
   const float* oscale; // [M][B] or null
   float alpha;
   int N, ohw;          // N = B*OH*OW
-  int kt_per_split, atomic;
+  int kt_per_split;
+  float* slab;         // split-K: per-split partial tiles [z][M][N] (null: single split)
 };
 
 struct WgradArgs {
@@ -119,7 +124,9 @@ struct WgradArgs {
   float* out;          // out[m*om + j*oj + t*ot]
   int om, oj, ot;
   float alpha;
-  int kt_per_split, splits, atomic;
+  int kt_per_split, splits, accumulate;
+  float* slab;         // split-K: per-split partial weights [split][numel(out)] (null: single split)
+  int out_numel;
 };
 
 template <int BM, int BN, int WGM, int WGN>
@@ -140,16 +147,17 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
   }
 }
 
-// One BK=16 K-step of MFMAs for a wave.  In step s lane half h supplies k = 8h + s.
-template <class C>
+// One 16-deep K-step of MFMAs for a wave over LDS tiles of row stride LD, starting at column
+// k0.  In step s lane half h supplies k = k0 + 8h + s.
+template <class C, int LD = LDK>
 __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
-                                          f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn) {
+                                          f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0 = 0) {
   const int r = lane & 31, h = lane >> 5;
   float a[C::TM][8], b[C::TN][8];
 #pragma unroll
-  for (int i = 0; i < C::TM; ++i) read_frag(As + ((wm * C::TM + i) * 32 + r) * LDK + 8 * h, a[i]);
+  for (int i = 0; i < C::TM; ++i) read_frag(As + ((wm * C::TM + i) * 32 + r) * LD + k0 + 8 * h, a[i]);
 #pragma unroll
-  for (int j = 0; j < C::TN; ++j) read_frag(Bs + ((wn * C::TN + j) * 32 + r) * LDK + 8 * h, b[j]);
+  for (int j = 0; j < C::TN; ++j) read_frag(Bs + ((wn * C::TN + j) * 32 + r) * LD + k0 + 8 * h, b[j]);
 #pragma unroll
   for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -261,13 +269,15 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     __syncthreads();
   }
 
-  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const bool add_bias = p.bias && blockIdx.z == 0;
+  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Split-K blocks store raw partial tiles to their slab; the reduce kernel applies the rest.
+  float* out = p.slab ? p.slab + (long)blockIdx.z * p.M * p.N : p.y;
+  const bool finish = p.slab == nullptr;
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
     const int n = n0 + (wn * C::TN + j) * 32 + (lane & 31);
     if (n >= p.N) continue;
-    const int b = p.oscale ? n / p.ohw : 0;
+    const int b = (finish && p.oscale) ? n / p.ohw : 0;
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
@@ -275,13 +285,11 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
         float v = p.alpha * acc[i][j][r];
-        if (p.oscale) v *= p.oscale[m * g.B + b];
-        if (add_bias) v += p.bias[m];
-        float* dst = p.y + (long)m * p.N + n;
-        if (p.atomic)
-          atomicAdd(dst, v);
-        else
-          *dst = v;
+        if (finish) {
+          if (p.oscale) v *= p.oscale[m * g.B + b];
+          if (p.bias) v += p.bias[m];
+        }
+        out[(long)m * p.N + n] = v;
       }
     }
   }
@@ -293,18 +301,18 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
 __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
-  constexpr int EA = BK * BM / kThreads;
-  constexpr int EB = BK * BN / kThreads;
-  constexpr int RSTEP = kThreads / BK;
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
+  constexpr int EA = BKW * BM / kThreads;
+  constexpr int EB = BKW * BN / kThreads;
+  constexpr int RSTEP = kThreads / BKW;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDKW];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDKW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int j0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int t = blockIdx.z / p.splits;
   const int split = blockIdx.z - t * p.splits;
-  const int kt_total = (p.K + BK - 1) / BK;
+  const int kt_total = (p.K + BKW - 1) / BKW;
   const int kt0 = split * p.kt_per_split;
   const int kt1 = min(kt_total, kt0 + p.kt_per_split);
   if (kt0 >= kt1) return;
@@ -312,8 +320,8 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
   const Gather& g = p.g;
   const int kh = t / g.KW, kw = t - kh * g.KW;
   const int cstride = g.B * g.H * g.W;
-  const int tk = tid % BK;   // k (pixel) fixed per thread for both operands
-  const int tr = tid / BK;   // row (m or j) base
+  const int tk = tid % BKW;   // k (pixel) fixed per thread for both operands
+  const int tr = tid / BKW;   // row (m or j) base
 
   const rsrc_t ra_r = make_rsrc(p.a, p.a_bytes);
   const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
@@ -322,7 +330,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
 
   float ra[EA], rb[EB], rsa[EA], rsb[EB];
   auto gload = [&](int kt) {
-    const int n = kt * BK + tk;
+    const int n = kt * BKW + tk;
     const bool nok = n < p.K;
     int b = 0, sp = -1;
     if (nok) {
@@ -349,9 +357,9 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][(tr + e * RSTEP) * LDK + tk] = SCALED ? ra[e] * rsa[e] : ra[e];
+    for (int e = 0; e < EA; ++e) As[buf][(tr + e * RSTEP) * LDKW + tk] = SCALED ? ra[e] * rsa[e] : ra[e];
 #pragma unroll
-    for (int e = 0; e < EB; ++e) Bs[buf][(tr + e * RSTEP) * LDK + tk] = SCALED ? rb[e] * rsb[e] : rb[e];
+    for (int e = 0; e < EB; ++e) Bs[buf][(tr + e * RSTEP) * LDKW + tk] = SCALED ? rb[e] * rsb[e] : rb[e];
   };
 
   f32x16 acc[C::TM][C::TN];
@@ -364,7 +372,8 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn);
+    mfma_tile<C, LDKW>(As[buf], Bs[buf], acc, lane, wm, wn, 0);
+    mfma_tile<C, LDKW>(As[buf], Bs[buf], acc, lane, wm, wn, 16);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -379,12 +388,14 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
-        float* dst = p.out + m * p.om + jj * p.oj + t * p.ot;
+        const int o = m * p.om + jj * p.oj + t * p.ot;
         const float v = p.alpha * acc[i][j][r];
-        if (p.atomic)
-          atomicAdd(dst, v);
+        if (p.slab)
+          p.slab[(long)split * p.out_numel + o] = v;
+        else if (p.accumulate)
+          p.out[o] += v;   // single split: this block is the element's only writer
         else
-          *dst = v;
+          p.out[o] = v;
       }
     }
   }
@@ -417,78 +428,157 @@ __global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict_
 // ------------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
-hipError_t launch_conv(ConvArgs p, hipStream_t st) {
-  const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
-  const int nct = (p.Ck + BK - 1) / BK;
-  const int kt_total = nct * p.T;
+// Tuning knobs (read once): target number of workgroups the split-K heuristics aim for.
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+int conv_block_target() {
+  static const int v = env_int("GANAMD_CONV_BLOCKS", 1024);
+  return v;
+}
+int wgrad_block_target() {
+  static const int v = env_int("GANAMD_WGRAD_BLOCKS", 1024);
+  return v;
+}
+
+
+// Split-K planning.  Splits exist only to fill the chip when the output tile grid is small;
+// each split writes its own slab (no atomics: deterministic, no contention) and a reduce
+// kernel folds the slabs.  The plan is a pure function of the geometry so the workspace query
+// and the launch agree.
+struct Plan {
+  int bm, bn, splits, kt_per_split;
+};
+
+int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
+int conv_bn(int bm) { return bm == 32 ? 256 : 128; }
+int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
+
+Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_splits) {
   int splits = 1;
-  const int blocks = gx * gy;
-  if (blocks < 1024 && kt_total >= 8) {
-    splits = (1024 + blocks - 1) / blocks;
-    splits = min(splits, max(1, kt_total / 4));
+  if (tiles < target && kt_total >= 8) splits = std::min((target + tiles - 1) / tiles, std::max(1, kt_total / 4));
+  splits = std::min(splits, max_splits);
+  const int per = (kt_total + splits - 1) / splits;
+  splits = (kt_total + per - 1) / per;
+  return Plan{bm, bn, splits, per};
+}
+
+Plan conv_plan(int M, int N, int Ck, int T) {
+  const int bm = conv_bm(M), bn = conv_bn(bm);
+  const int tiles = ((N + bn - 1) / bn) * ((M + bm - 1) / bm);
+  return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, conv_block_target(), 16);
+}
+
+Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
+  int bm = wgrad_bm(M, scaled), bn = 128;
+  if (J <= 64 && bm >= 64) {  // narrow gathered side: a 64x64 tile wastes nothing on J = 48..64
+    bm = 64;
+    bn = 64;
   }
-  p.kt_per_split = (kt_total + splits - 1) / splits;
-  splits = (kt_total + p.kt_per_split - 1) / p.kt_per_split;
-  p.atomic = splits > 1;
-  if (p.atomic) {
-    hipError_t e = hipMemsetAsync(p.y, 0, sizeof(float) * (size_t)p.M * p.N, st);
-    if (e != hipSuccess) return e;
+  const int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
+  return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, wgrad_block_target(), 32);
+}
+
+__global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int N, int ohw, int B,
+                                         const float* __restrict__ oscale, const float* __restrict__ bias,
+                                         float* __restrict__ y) {
+  const long total = (long)M * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += slab[s * total + i];
+    const int m = (int)(i / N);
+    if (oscale) v *= oscale[m * B + (int)(i % N) / ohw];
+    if (bias) v += bias[m];
+    y[i] = v;
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3(gx, gy, splits), dim3(kThreads), 0,
+}
+
+__global__ void wgrad_split_reduce_kernel(const float* __restrict__ slab, int S, int total, float* __restrict__ out,
+                                          int accumulate) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += slab[(long)s * total + i];
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
+int grid1d(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+hipError_t launch_conv(ConvArgs p, const Plan& pl, float* slab, hipStream_t st) {
+  const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
+  p.kt_per_split = pl.kt_per_split;
+  p.slab = pl.splits > 1 ? slab : nullptr;
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3(gx, gy, pl.splits), dim3(kThreads), 0,
                      st, p);
+  if (pl.splits > 1)
+    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.N)), dim3(256), 0, st, slab, pl.splits,
+                       p.M, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.y);
   return hipGetLastError();
 }
 
 template <int MODE, bool BSCALE>
-hipError_t dispatch_conv_tile(const ConvArgs& p, hipStream_t st) {
-  if (p.M <= 32) return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, st);
-  if (p.M <= 64) return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, st);
-  if (p.M <= 96) return launch_conv<96, 128, 1, 4, MODE, BSCALE>(p, st);
-  return launch_conv<128, 128, 2, 2, MODE, BSCALE>(p, st);
+hipError_t dispatch_conv_tile(const ConvArgs& p, const Plan& pl, float* slab, hipStream_t st) {
+  switch (pl.bm) {
+    case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
+    case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
+    case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE>(p, pl, slab, st);
+    default: return launch_conv<128, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
+  }
 }
 
-hipError_t dispatch_conv(const ConvArgs& p, hipStream_t st) {
+hipError_t dispatch_conv(const ConvArgs& p, float* slab, hipStream_t st) {
+  const Plan pl = conv_plan(p.M, p.N, p.Ck, p.T);
+  if (pl.splits > 1 && !slab) return hipErrorInvalidValue;
   const bool s = p.g.scale != nullptr;
   switch (p.g.mode) {
-    case kZero: return s ? dispatch_conv_tile<kZero, true>(p, st) : dispatch_conv_tile<kZero, false>(p, st);
+    case kZero:
+      return s ? dispatch_conv_tile<kZero, true>(p, pl, slab, st) : dispatch_conv_tile<kZero, false>(p, pl, slab, st);
     case kReplicate:
-      return s ? dispatch_conv_tile<kReplicate, true>(p, st) : dispatch_conv_tile<kReplicate, false>(p, st);
+      return s ? dispatch_conv_tile<kReplicate, true>(p, pl, slab, st)
+               : dispatch_conv_tile<kReplicate, false>(p, pl, slab, st);
     default:
-      return s ? dispatch_conv_tile<kTransposed, true>(p, st) : dispatch_conv_tile<kTransposed, false>(p, st);
+      return s ? dispatch_conv_tile<kTransposed, true>(p, pl, slab, st)
+               : dispatch_conv_tile<kTransposed, false>(p, pl, slab, st);
   }
 }
 
 template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
-hipError_t launch_wgrad(WgradArgs p, int T, hipStream_t st) {
+hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStream_t st) {
   const int gx = (p.J + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
-  const int kt_total = (p.K + BK - 1) / BK;
-  const int blocks = gx * gy * T;
-  int splits = 1;
-  if (blocks < 1024) splits = min((1024 + blocks - 1) / blocks, max(1, kt_total / 8));
-  p.kt_per_split = (kt_total + splits - 1) / splits;
-  splits = (kt_total + p.kt_per_split - 1) / p.kt_per_split;
-  p.splits = splits;
-  p.atomic = 1;
-  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED>), dim3(gx, gy, T * splits), dim3(kThreads), 0,
-                     st, p);
+  p.kt_per_split = pl.kt_per_split;
+  p.splits = pl.splits;
+  p.slab = pl.splits > 1 ? slab : nullptr;
+  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED>), dim3(gx, gy, T * pl.splits), dim3(kThreads),
+                     0, st, p);
+  if (pl.splits > 1)
+    hipLaunchKernelGGL(wgrad_split_reduce_kernel, dim3(grid1d(p.out_numel)), dim3(256), 0, st, slab, pl.splits,
+                       p.out_numel, p.out, p.accumulate);
   return hipGetLastError();
 }
 
 template <int MODE, bool SCALED>
-hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, hipStream_t st) {
-  if (p.M <= 32) return launch_wgrad<32, 128, 1, 4, MODE, SCALED>(p, T, st);
-  if (p.M <= 64) return launch_wgrad<64, 128, 2, 2, MODE, SCALED>(p, T, st);
-  if (p.M <= 96) return launch_wgrad<96, 128, 1, 4, MODE, SCALED>(p, T, st);
-  return launch_wgrad<128, 128, 2, 2, MODE, SCALED>(p, T, st);
+hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, const Plan& pl, float* slab, hipStream_t st) {
+  if (pl.bn == 64) return launch_wgrad<64, 64, 2, 2, MODE, SCALED>(p, T, pl, slab, st);
+  switch (pl.bm) {
+    case 32: return launch_wgrad<32, 128, 1, 4, MODE, SCALED>(p, T, pl, slab, st);
+    case 64: return launch_wgrad<64, 128, 2, 2, MODE, SCALED>(p, T, pl, slab, st);
+    case 96: return launch_wgrad<96, 128, 1, 4, MODE, SCALED>(p, T, pl, slab, st);
+    default: return launch_wgrad<128, 128, 2, 2, MODE, SCALED>(p, T, pl, slab, st);
+  }
 }
 
-hipError_t dispatch_wgrad(const WgradArgs& p, int T, hipStream_t st) {
+hipError_t dispatch_wgrad(const WgradArgs& p, int T, float* slab, hipStream_t st) {
   const bool s = p.ascale != nullptr || p.g.scale != nullptr;
   if (s && !(p.ascale && p.g.scale)) return hipErrorInvalidValue;  // both scales or none
+  const Plan pl = wgrad_plan(p.M, p.J, p.K, T, s);
+  if (pl.splits > 1 && !slab) return hipErrorInvalidValue;
   if (p.g.mode == kReplicate)
-    return s ? dispatch_wgrad_tile<kReplicate, true>(p, T, st) : dispatch_wgrad_tile<kReplicate, false>(p, T, st);
-  return s ? dispatch_wgrad_tile<kZero, true>(p, T, st) : dispatch_wgrad_tile<kZero, false>(p, T, st);
+    return s ? dispatch_wgrad_tile<kReplicate, true>(p, T, pl, slab, st)
+             : dispatch_wgrad_tile<kReplicate, false>(p, T, pl, slab, st);
+  return s ? dispatch_wgrad_tile<kZero, true>(p, T, pl, slab, st)
+           : dispatch_wgrad_tile<kZero, false>(p, T, pl, slab, st);
 }
 
 bool desc_ok(const ganamd_conv_desc* d) {
@@ -500,21 +590,62 @@ bool desc_ok(const ganamd_conv_desc* d) {
 
 extern "C" {
 
+// Geometry of each GEMM the three entry points issue (shared by the workspace query and launch).
+static void fwd_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T) {
+  *M = d->Cout;
+  *N = d->B * d->OH * d->OW;
+  *Ck = d->Cin;
+  *T = d->KH * d->KW;
+}
+
+static void dgrad_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T) {
+  *M = d->Cin;
+  *Ck = d->Cout;
+  *T = d->KH * d->KW;
+  const int hp = d->transposed ? d->H : d->H + 2 * d->pad, wp = d->transposed ? d->W : d->W + 2 * d->pad;
+  *N = d->B * hp * wp;
+}
+
+static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
+  if (d->transposed || d->pad == 0) return 0;
+  return sizeof(float) * (size_t)d->Cin * d->B * (d->H + 2 * d->pad) * (d->W + 2 * d->pad);
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
 int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   if (!desc_ok(d) || !bytes) return GANAMD_EINVAL;
+  int M, N, Ck, T;
   *bytes = 0;
-  if (op == GANAMD_CONV_DGRAD && !d->transposed && d->pad > 0) {
-    const size_t hp = d->H + 2 * d->pad, wp = d->W + 2 * d->pad;
-    *bytes = sizeof(float) * (size_t)d->Cin * d->B * hp * wp;
+  if (op == GANAMD_CONV_FWD) {
+    fwd_gemm(d, &M, &N, &Ck, &T);
+    const Plan pl = conv_plan(M, N, Ck, T);
+    *bytes = pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0;
+  } else if (op == GANAMD_CONV_DGRAD) {
+    dgrad_gemm(d, &M, &N, &Ck, &T);
+    const Plan pl = conv_plan(M, N, Ck, T);
+    *bytes = align256(dgrad_pad_bytes(d)) + (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
+  } else if (op == GANAMD_CONV_WGRAD) {
+    const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
+    T = d->KH * d->KW;
+    const int Mw = d->transposed ? d->Cin : d->Cout, Jw = d->transposed ? d->Cout : d->Cin;
+    // the modulated (scaled) variant plans the same or more splits; size for the larger
+    const Plan a = wgrad_plan(Mw, Jw, Kpix, T, false), b = wgrad_plan(Mw, Jw, Kpix, T, true);
+    const int S = std::max(a.splits, b.splits);
+    *bytes = S > 1 ? sizeof(float) * (size_t)S * d->Cin * d->Cout * T : 0;
+  } else {
+    return GANAMD_EINVAL;
   }
   return GANAMD_OK;
 }
 
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
-                    const float* x_scale, const float* y_scale, float alpha, float* y, hipStream_t stream) {
+                    const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
+                    hipStream_t stream) {
   if (!desc_ok(d) || !x || !w || !y) return GANAMD_EINVAL;
   ConvArgs p{};
-  const int T = d->KH * d->KW;
+  int M, N, Ck, T;
+  fwd_gemm(d, &M, &N, &Ck, &T);
   p.w = w;
   if (d->transposed) {  // weights [Cin][Cout][KH][KW]
     p.sm = T;
@@ -525,8 +656,8 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
   }
   p.st = 1;
   p.w_bytes = 4 * d->Cin * d->Cout * T;
-  p.M = d->Cout;
-  p.Ck = d->Cin;
+  p.M = M;
+  p.Ck = Ck;
   p.T = T;
   p.g = Gather{x, x_scale, d->Cin, d->B, d->H, d->W, d->OH, d->OW, d->KW, d->stride, d->pad,
                d->transposed ? kTransposed : (d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero)};
@@ -534,59 +665,61 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
   p.bias = bias;
   p.oscale = y_scale;
   p.alpha = alpha;
-  p.N = d->B * d->OH * d->OW;
+  p.N = N;
   p.ohw = d->OH * d->OW;
-  return dispatch_conv(p, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  return dispatch_conv(p, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale, float alpha,
                       float* gx, void* workspace, hipStream_t stream) {
   if (!desc_ok(d) || !gy || !w || !gx) return GANAMD_EINVAL;
-  const int T = d->KH * d->KW;
+  int M, N, Ck, T;
+  dgrad_gemm(d, &M, &N, &Ck, &T);
   ConvArgs p{};
   p.w = w;
   p.st = 1;
   p.w_bytes = 4 * d->Cin * d->Cout * T;
-  p.M = d->Cin;
-  p.Ck = d->Cout;
+  p.M = M;
+  p.Ck = Ck;
   p.T = T;
   p.bias = nullptr;
   p.oscale = nullptr;
   p.alpha = alpha;
+  p.N = N;
+  const size_t pad_bytes = dgrad_pad_bytes(d);
+  char* ws = static_cast<char*>(workspace);
+  float* slab = ws ? reinterpret_cast<float*>(ws + align256(pad_bytes)) : nullptr;
   if (d->transposed) {
     // dX of ConvT = plain zero-padded conv of gy with W viewed [Cin][Cout][KH][KW]
     p.sm = d->Cout * T;
     p.sc = T;
     p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, kZero};
     p.y = gx;
-    p.N = d->B * d->H * d->W;
     p.ohw = d->H * d->W;
-    return dispatch_conv(p, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+    return dispatch_conv(p, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   // dX of conv = transposed gather of gy into the padded input frame, then fold the pad
   p.sm = T;
   p.sc = d->Cin * T;
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
-  float* out = d->pad > 0 ? static_cast<float*>(workspace) : gx;
-  if (d->pad > 0 && !workspace) return GANAMD_EINVAL;
+  if (pad_bytes && !ws) return GANAMD_EINVAL;
+  float* out = pad_bytes ? reinterpret_cast<float*>(ws) : gx;
   p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
   p.y = out;
-  p.N = d->B * Hp * Wp;
   p.ohw = Hp * Wp;
-  if (dispatch_conv(p, stream) != hipSuccess) return GANAMD_ELAUNCH;
-  if (d->pad > 0) {
+  if (dispatch_conv(p, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+  if (pad_bytes) {
     const long planes = (long)d->Cin * d->B;
-    const long total = planes * d->H * d->W;
-    const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(fold_pad_kernel, dim3(blocks), dim3(256), 0, stream, out, gx, planes, d->H, d->W, d->pad,
-                       d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
+    hipLaunchKernelGGL(fold_pad_kernel, dim3(grid1d(planes * d->H * d->W)), dim3(256), 0, stream, out, gx, planes,
+                       d->H, d->W, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
     if (hipGetLastError() != hipSuccess) return GANAMD_ELAUNCH;
   }
   return GANAMD_OK;
 }
 
 int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
-                      const float* gy_scale, float alpha, float* gw, int accumulate, hipStream_t stream) {
+                      const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
+                      hipStream_t stream) {
   if (!desc_ok(d) || !x || !gy || !gw) return GANAMD_EINVAL;
   if ((x_scale == nullptr) != (gy_scale == nullptr)) return GANAMD_EINVAL;
   const int T = d->KH * d->KW;
@@ -622,11 +755,9 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
     p.oj = T;
   }
   p.out = gw;
-  const size_t wsz = sizeof(float) * (size_t)d->Cin * d->Cout * T;
-  if (!accumulate) {
-    if (hipMemsetAsync(gw, 0, wsz, stream) != hipSuccess) return GANAMD_ELAUNCH;
-  }
-  return dispatch_wgrad(p, T, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  p.out_numel = d->Cin * d->Cout * T;
+  p.accumulate = accumulate;
+  return dispatch_wgrad(p, T, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 }  // extern "C"

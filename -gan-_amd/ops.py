@@ -52,12 +52,17 @@ class Geo:
         return d
 
     def ws_bytes(self, op):
-        n = _lib.c_size_t(0)
-        check(LIB.ganamd_conv_workspace(self.desc(), op, n), "conv_workspace")
-        return n.value
+        key = (self, op)
+        v = _WS_CACHE.get(key)
+        if v is None:
+            n = _lib.c_size_t(0)
+            check(LIB.ganamd_conv_workspace(self.desc(), op, n), "conv_workspace")
+            v = _WS_CACHE[key] = n.value
+        return v
 
 
 _DESC_CACHE: dict = {}
+_WS_CACHE: dict = {}
 
 
 def conv_geo(B, cin, h, w, cout, k, stride=1, pad=0, pad_mode=_lib.PAD_REPLICATE):
@@ -113,8 +118,10 @@ def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0):
     _need(ys, geo.Cout * geo.B, "conv_fwd y_scale")
     FlopCounter.add(geo, "fwd", xs is not None, ys is not None)
     y = torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device, dtype=torch.float32)
+    nb = geo.ws_bytes(_lib.CONV_FWD)
+    ws = workspace(nb, x.device) if nb else None
     check(LIB.ganamd_conv_fwd(geo.desc(), ptr(x), ptr(w), ptr(bias), ptr(xs), ptr(ys), float(alpha), ptr(y),
-                              stream()), "conv_fwd")
+                              ptr(ws), stream()), "conv_fwd")
     return y
 
 
@@ -140,8 +147,10 @@ def _conv_wgrad(geo: Geo, x, gy, xs=None, gys=None, alpha=1.0, out=None, accumul
     FlopCounter.add(geo, "wgrad", xs is not None, gys is not None)
     shape = (geo.Cin, geo.Cout, geo.K, geo.K) if geo.transposed else (geo.Cout, geo.Cin, geo.K, geo.K)
     gw = out if out is not None else torch.empty(shape, device=x.device, dtype=torch.float32)
+    nb = geo.ws_bytes(_lib.CONV_WGRAD)
+    ws = workspace(nb, x.device) if nb else None
     check(LIB.ganamd_conv_wgrad(geo.desc(), ptr(x), ptr(gy), ptr(xs), ptr(gys), float(alpha), ptr(gw),
-                                int(accumulate), stream()), "conv_wgrad")
+                                int(accumulate), ptr(ws), stream()), "conv_wgrad")
     return gw
 
 

@@ -60,9 +60,11 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
  *   grouped conv with per-sample weights W*c*s*d (generator_13_5.py:234-248) via x_scale = s,
  *   y_scale = d; nn.ConvTranspose2d (generator_13_5.py:156,594) with transposed=1;
  *   EqualizedLinear = F.linear (generator_13_5.py:25-26, discriminator_9_4.py:26-27).
- * x_scale, y_scale, bias may be NULL. */
+ * x_scale, y_scale, bias may be NULL.  Workspace: ganamd_conv_workspace(d, GANAMD_CONV_FWD)
+ * (split-K partial tiles when the output grid is too small to fill the chip; may be 0). */
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
-                    const float* x_scale, const float* y_scale, float alpha, float* y, hipStream_t stream);
+                    const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
+                    hipStream_t stream);
 
 /* gx = alpha * dConv/dx applied to (gy * gy_scale[co][b]), including the ReplicationPad2d
  * backward (edge folding).  Replaces aten convolution_backward (input grad) + replication_pad2d_backward.
@@ -70,10 +72,12 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale,
                       float alpha, float* gx, void* workspace, hipStream_t stream);
 
-/* gw (+)= alpha * dConv/dW for inputs (x * x_scale) and (gy * gy_scale).  accumulate=0
- * overwrites gw.  Replaces aten convolution_backward (weight grad). */
+/* gw (+)= alpha * dConv/dW for inputs (x * x_scale) and (gy * gy_scale) (both scales or
+ * neither).  accumulate=0 overwrites gw.  Replaces aten convolution_backward (weight grad).
+ * Workspace: ganamd_conv_workspace(d, GANAMD_CONV_WGRAD).  Deterministic (no atomics). */
 int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
-                      const float* gy_scale, float alpha, float* gw, int accumulate, hipStream_t stream);
+                      const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
+                      hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Train-mode BatchNorm (1d or 2d) fused with an optional per-channel PReLU.

@@ -44,7 +44,7 @@ def test_invalid_arguments_rejected():
     d = _lib.ConvDesc(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)   # B = 0: invalid geometry
     n = _lib.c_size_t(0)
     assert L.ganamd_conv_workspace(d, 0, n) == -1
-    assert L.ganamd_conv_fwd(d, None, None, None, None, None, 1.0, None, None) == -1
+    assert L.ganamd_conv_fwd(d, None, None, None, None, None, 1.0, None, None, None) == -1
     assert L.ganamd_prelu_fwd(None, None, 0, 0, None, None) == -1
     assert L.ganamd_adamw(None, None, None, None, 0, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, None) == -1
 
@@ -55,7 +55,7 @@ def test_workspace_sizes():
     d = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0)
     n = _lib.c_size_t(0)
     assert L.ganamd_conv_workspace(d, _lib.CONV_DGRAD, n) == 0
-    assert n.value == 4 * 8 * 4 * 18 * 18
+    assert n.value >= 4 * 8 * 4 * 18 * 18
     assert L.ganamd_rowreduce_workspace(8, 4096) >= 8 * 3 * 4
 
 
