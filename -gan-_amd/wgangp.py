@@ -58,13 +58,18 @@ class Train:
 
     def generator_trainstep(self, b_size):
         """train/wgangp.py:20-27."""
+        gen_imgs, g_loss = self.generator_backward(b_size)
+        self.optimizer_G.step()
+        return gen_imgs, g_loss
+
+    def generator_backward(self, b_size):
+        """generator_trainstep up to (not including) the optimizer step."""
         self.optimizer_G.zero_grad()
         z = self.rng.randn((b_size, self.nz, 1, 1))
         gen_imgs = self._generate(z)
         with _frozen(self.discriminator):
             g_loss = -torch.mean(self.discriminator(gen_imgs))
             g_loss.backward()
-        self.optimizer_G.step()
         return gen_imgs, g_loss
 
     def discriminator_loss(self, real_pred, fake_pred):
@@ -89,6 +94,12 @@ class Train:
 
     def discriminator_trainstep(self, images, b_size):
         """train/wgangp.py:56-71."""
+        out = self.discriminator_backward(images, b_size)
+        self.optimizer_D.step()
+        return out
+
+    def discriminator_backward(self, images, b_size):
+        """discriminator_trainstep up to (not including) the optimizer step."""
         self.optimizer_D.zero_grad()
         z = self.rng.randn((b_size, self.nz, 1, 1))
         with torch.no_grad():
@@ -103,7 +114,6 @@ class Train:
         fake_loss.backward()
         gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
         gp.backward()
-        self.optimizer_D.step()
         return real_loss, fake_loss, gp
 
     def train(self):

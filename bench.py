@@ -45,20 +45,25 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=64, help="images per GPU")
-    ap.add_argument("--mode", choices=["eager", "graph"], default="eager")
+    ap.add_argument("--mode", choices=["eager", "graph"], default="graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
     return ap.parse_args()
 
 
-def setup_dist(n):
+def setup_dist(n, backend):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":      # every rank on cuda:0 (rehearsal of the N>1 path on one GPU)
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     assert world == n or world == 1, f"--gpus {n} but WORLD_SIZE {world}"
@@ -91,18 +96,18 @@ def cpu_baseline(threads):
 
 def main():
     args = parse()
-    world, rank, local = setup_dist(args.gpus)
+    world, rank, local = setup_dist(args.gpus, args.backend)
     dev = torch.device("cuda", torch.cuda.current_device())
     import gan_amd
     from gan_amd import ops
-    from gan_amd.dist import attach_grad_sync
+    from gan_amd.dist import allreduce_mean_, attach_grad_sync
 
     torch.manual_seed(1234)                         # identical initial weights on every rank
     G = gan_amd.Generator(256).to(dev)
     D = gan_amd.Discriminator().to(dev)
     torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
     tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev))
-    if world > 1:
+    if world > 1 and args.mode == "eager":
         attach_grad_sync(tr.optimizer_G)
         attach_grad_sync(tr.optimizer_D)
     B = args.batch
@@ -112,6 +117,23 @@ def main():
             images = torch.randn(B, 3, 64, 64, device=dev)
             tr.discriminator_trainstep(images, B)
         tr.generator_trainstep(B)
+
+    def sync(opt):
+        if world > 1:
+            allreduce_mean_(opt.flat.grad)
+
+    def iteration_split():
+        # the same iteration with the gradient all-reduce outside the optimizer (graph mode)
+        for _ in range(N_CRITIC):
+            tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B)
+            sync(tr.optimizer_D)
+            tr.optimizer_D.step()
+        tr.generator_backward(B)
+        sync(tr.optimizer_G)
+        tr.optimizer_G.step()
+
+    if args.mode == "graph" and world > 1:
+        iteration = iteration_split
 
     # warm-up (eager); the first one also counts the conv FLOPs this build issues
     ops.FlopCounter.enabled = True
@@ -124,16 +146,46 @@ def main():
 
     step = iteration
     if args.mode == "graph":
-        graph = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            iteration()
-        torch.cuda.current_stream().wait_stream(s)
-        with torch.cuda.graph(graph):
-            iteration()
-        torch.cuda.synchronize()
-        step = graph.replay
+        # one HIP graph per critic step and one per generator step (the synthetic real batch,
+        # z, noise and eps are drawn inside the graphs; torch advances the Philox offsets on
+        # every replay), replayed 5 + 1 times per iteration
+        # With N > 1 ranks the RCCL all-reduce of the flat gradient runs eagerly between a
+        # forward/backward graph and an optimizer graph (collectives are kept out of capture).
+        def capture(fn):
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fn()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            return g
+
+        if world == 1:
+            gd = capture(lambda: tr.discriminator_trainstep(torch.randn(B, 3, 64, 64, device=dev), B))
+            gg = capture(lambda: tr.generator_trainstep(B))
+            torch.cuda.synchronize()
+
+            def step():
+                for _ in range(N_CRITIC):
+                    gd.replay()
+                gg.replay()
+        else:
+            gd = capture(lambda: tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B))
+            gdo = capture(tr.optimizer_D.step)
+            gg = capture(lambda: tr.generator_backward(B))
+            ggo = capture(tr.optimizer_G.step)
+            torch.cuda.synchronize()
+
+            def step():
+                for _ in range(N_CRITIC):
+                    gd.replay()
+                    allreduce_mean_(tr.optimizer_D.flat.grad)
+                    gdo.replay()
+                gg.replay()
+                allreduce_mean_(tr.optimizer_G.flat.grad)
+                ggo.replay()
 
     if world > 1:
         dist.barrier()
