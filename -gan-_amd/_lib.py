@@ -22,12 +22,19 @@ c_size_t = ctypes.c_size_t
 vp = ctypes.c_void_p
 
 PAD_ZERO, PAD_REPLICATE = 0, 1
+EPI_STORE, EPI_BIAS, EPI_DEMOD, EPI_ACCUM, EPI_SCALE = 0, 1, 2, 3, 4
 CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
 
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("B", "Cin", "H", "W", "Cout", "OH", "OW", "KH", "KW", "stride", "pad", "pad_mode", "transposed")]
+
+
+class GTile(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("a_off", "lda", "b_off", "ldb", "c_off", "ldc", "rows", "cols", "K", "epi", "bias_off")] + \
+               [("scale", ctypes.c_float)]
 
 
 # name -> (restype, argtypes)
@@ -48,6 +55,7 @@ _SIGS = {
     "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, vp, vp]),
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),
     "ganamd_adamw": (c_int, [vp, vp, vp, vp, c_long, vp, c_float, c_float, c_float, c_float, c_float, vp]),
+    "ganamd_grouped_gemm": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -180,27 +180,28 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
 // ------------------------------------------------------------------------------------------
 // forward / dgrad / transposed: K = (tap, channel), N = output pixels
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, int KS>
 __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
+  constexpr int LD = KS + 2;
   using C = TileCfg<BM, BN, WGM, WGN>;
-  constexpr int EA = BK * BM / kThreads;
-  constexpr int EB = BK * BN / kThreads;
+  constexpr int EA = KS * BM / kThreads;
+  constexpr int EB = KS * BN / kThreads;
   static_assert(kThreads % BN == 0, "B mapping: n fixed per thread");
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LD];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int nct = (p.Ck + BK - 1) / BK;
+  const int nct = (p.Ck + KS - 1) / KS;
   const int kt_total = nct * p.T;
   const int kt0 = blockIdx.z * p.kt_per_split;
   const int kt1 = min(kt_total, kt0 + p.kt_per_split);
   if (kt0 >= kt1) return;
 
   // A mapping: k fixed per thread, m strided.  B mapping: n fixed per thread, k strided.
-  const int a_k = tid % BK, a_m = tid / BK;
-  constexpr int A_MSTEP = kThreads / BK;
+  const int a_k = tid % KS, a_m = tid / KS;
+  constexpr int A_MSTEP = kThreads / KS;
   const int b_n = tid % BN, b_k = tid / BN;
   constexpr int B_KSTEP = kThreads / BN;
 
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 
   auto gload = [&](int kt) {
     const int t = kt / nct;
-    const int c0 = (kt - t * nct) * BK;
+    const int c0 = (kt - t * nct) * KS;
     if (t != cur_t) {
       cur_t = t;
       const int kh = t / g.KW;
@@ -249,9 +250,9 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][(a_m + e * A_MSTEP) * LDK + a_k] = ra[e];
+    for (int e = 0; e < EA; ++e) As[buf][(a_m + e * A_MSTEP) * LD + a_k] = ra[e];
 #pragma unroll
-    for (int e = 0; e < EB; ++e) Bs[buf][b_n * LDK + b_k + e * B_KSTEP] = BSCALE ? rb[e] * rs[e] : rb[e];
+    for (int e = 0; e < EB; ++e) Bs[buf][b_n * LD + b_k + e * B_KSTEP] = BSCALE ? rb[e] * rs[e] : rb[e];
   };
 
   f32x16 acc[C::TM][C::TN];
@@ -264,7 +265,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn);
+#pragma unroll
+    for (int k0 = 0; k0 < KS; k0 += 16) mfma_tile<C, LD>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -433,6 +435,10 @@ int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
+int conv_ks() {
+  static const int v = env_int("GANAMD_CONV_KS", 16);
+  return v;
+}
 int conv_block_target() {
   static const int v = env_int("GANAMD_CONV_BLOCKS", 1024);
   return v;
@@ -448,7 +454,7 @@ int wgrad_block_target() {
 // kernel folds the slabs.  The plan is a pure function of the geometry so the workspace query
 // and the launch agree.
 struct Plan {
-  int bm, bn, splits, kt_per_split;
+  int bm, bn, splits, kt_per_split, ks = 16;
 };
 
 int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
@@ -457,7 +463,11 @@ int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96
 
 Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_splits) {
   int splits = 1;
-  if (tiles < target && kt_total >= 8) splits = std::min((target + tiles - 1) / tiles, std::max(1, kt_total / 4));
+  // a GEMM whose whole K loop is short is launch-bound: one more launch for the reduce costs
+  // more than the idle CUs (the 519 per-conv style MLPs are this case)
+  const long work = (long)tiles * kt_total;
+  if (tiles < target && kt_total >= 16 && work >= 4096)
+    splits = std::min((target + tiles - 1) / tiles, std::max(1, kt_total / 8));
   splits = std::min(splits, max_splits);
   const int per = (kt_total + splits - 1) / splits;
   splits = (kt_total + per - 1) / per;
@@ -465,9 +475,11 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_spl
 }
 
 Plan conv_plan(int M, int N, int Ck, int T) {
-  const int bm = conv_bm(M), bn = conv_bn(bm);
+  const int bm = conv_bm(M), bn = conv_bn(bm), ks = conv_ks();
   const int tiles = ((N + bn - 1) / bn) * ((M + bm - 1) / bm);
-  return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, conv_block_target(), 16);
+  Plan pl = split_plan(bm, bn, tiles, ((Ck + ks - 1) / ks) * T, conv_block_target(), 16);
+  pl.ks = ks;
+  return pl;
 }
 
 Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
@@ -510,8 +522,12 @@ hipError_t launch_conv(ConvArgs p, const Plan& pl, float* slab, hipStream_t st) 
   const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
   p.kt_per_split = pl.kt_per_split;
   p.slab = pl.splits > 1 ? slab : nullptr;
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3(gx, gy, pl.splits), dim3(kThreads), 0,
-                     st, p);
+  if (pl.ks == 32)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, 32>), dim3(gx, gy, pl.splits), dim3(kThreads),
+                       0, st, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, 16>), dim3(gx, gy, pl.splits), dim3(kThreads),
+                       0, st, p);
   if (pl.splits > 1)
     hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.N)), dim3(256), 0, st, slab, pl.splits,
                        p.M, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.y);

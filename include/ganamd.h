@@ -146,6 +146,28 @@ int ganamd_segment_sumsq(const float* w, long rows, int T, float* out, hipStream
 int ganamd_adamw(float* p, const float* g, float* m, float* v, long n, int32_t* step, float lr, float beta1,
                  float beta2, float eps, float weight_decay, hipStream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Grouped small GEMMs over a static tile list (the generator's style bank: the 519 per-conv
+ * style MLPs and demodulation products of generator_13_5.py:223-227,239-242 in one launch).
+ *   C[c_off + r*ldc + n] (=|+=) epi( sum_k A(r,k) * B(k,n) ),  r < rows, n < cols (each <= 64)
+ *   A(r,k) = a_trans ? A[a_off + k*lda + r] : A[a_off + r*lda + k]
+ *   B(k,n) = b_trans ? B[b_off + n*ldb + k] : B[b_off + k*ldb + n]   (squared if b_square)
+ * ------------------------------------------------------------------------------------- */
+#define GANAMD_EPI_STORE 0
+#define GANAMD_EPI_BIAS 1   /* scale*acc + bias[bias_off + r] */
+#define GANAMD_EPI_DEMOD 2  /* rsqrt(scale^2 * acc + 1e-8) */
+#define GANAMD_EPI_ACCUM 3  /* C += scale*acc */
+#define GANAMD_EPI_SCALE 4  /* scale*acc */
+
+typedef struct ganamd_gtile {
+  int32_t a_off, lda, b_off, ldb, c_off, ldc;
+  int32_t rows, cols, K, epi, bias_off;
+  float scale;
+} ganamd_gtile;
+
+int ganamd_grouped_gemm(const float* A, const float* B, float* C, const float* bias, const ganamd_gtile* tiles,
+                        int n_tiles, int a_trans, int b_trans, int b_square, hipStream_t stream);
+
 /* Library identification (for load checks). */
 const char* ganamd_version(void);
 
