@@ -36,6 +36,21 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return sh[0] + sh[1] + sh[2] + sh[3];
 }
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
 inline int splits_for(long L) {
   long s = (L + kChunk - 1) / kChunk;
   if (s < 1) s = 1;
@@ -51,39 +66,56 @@ inline int grid_for(long n) {
 }
 
 // ---------------------------------------------------------------- BatchNorm statistics
+// Statistics and the backward's row sums accumulate in double, as torch's CPU BatchNorm does
+// (acc_type<float> on CPU is double): with B = 4..64 samples per BatchNorm1d channel the
+// normalisation is ill-conditioned and float accumulation measurably moves the result.
+//
 // block (s, c): chunk mean and M2 of row c (two passes over an L2-resident 16 KB chunk)
 __global__ __launch_bounds__(kNT) void bn_partial_kernel(const float* __restrict__ x, long L, int S,
-                                                         float* __restrict__ part) {
-  __shared__ float sh[4];
+                                                         double* __restrict__ part) {
+  __shared__ double sh[4];
   const int c = blockIdx.y, s = blockIdx.x;
   const long per = (L + S - 1) / S;
   const long lo = s * per, hi = min(L, lo + per);
   const float* row = x + (long)c * L;
-  float acc = 0.f;
+  double acc = 0.0;
   for (long i = lo + threadIdx.x; i < hi; i += kNT) acc += row[i];
-  const float n = (float)max(0L, hi - lo);
-  const float mean = n > 0 ? block_sum(acc, sh) / n : 0.f;
-  float m2 = 0.f;
+  const double n = (double)max(0L, hi - lo);
+  const double mean = n > 0 ? block_sum_d(acc, sh) / n : 0.0;
+  double m2 = 0.0;
   for (long i = lo + threadIdx.x; i < hi; i += kNT) {
-    const float d = row[i] - mean;
+    const double d = row[i] - mean;
     m2 += d * d;
   }
-  m2 = block_sum(m2, sh);
+  m2 = block_sum_d(m2, sh);
   if (threadIdx.x == 0) {
-    float* o = part + ((long)c * S + s) * 3;
+    double* o = part + ((long)c * S + s) * 3;
     o[0] = n;
     o[1] = mean;
     o[2] = m2;
   }
 }
 
+__device__ __forceinline__ void bn_store_stats(int c, double mean, double m2, long L, float* running_mean,
+                                               float* running_var, float momentum, float eps, float* save_mean,
+                                               float* save_invstd) {
+  const double var = m2 / (double)L;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+  if (running_var) {
+    const float unb = (float)(L > 1 ? m2 / (double)(L - 1) : var);
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  }
+}
+
 // Chan merge of the S partials, running-stat update, invstd.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int C, int S, long L, float* running_mean,
+__global__ void bn_finalize_kernel(const double* __restrict__ part, int C, int S, long L, float* running_mean,
                                    float* running_var, float momentum, float eps, float* save_mean,
                                    float* save_invstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const float* p = part + (long)c * S * 3;
+  const double* p = part + (long)c * S * 3;
   double n = 0, mean = 0, m2 = 0;
   for (int s = 0; s < S; ++s) {
     const double nb = p[3 * s], mb = p[3 * s + 1], m2b = p[3 * s + 2];
@@ -93,13 +125,105 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int C, int S,
     m2 += m2b + d * d * n * nb / nn;
     n = nn;
   }
-  const float var = (float)(m2 / (double)L);
-  save_mean[c] = (float)mean;
-  save_invstd[c] = 1.0f / sqrtf(var + eps);
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-  if (running_var) {
-    const float unb = L > 1 ? (float)(m2 / (double)(L - 1)) : var;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
+}
+
+// Short rows (BatchNorm1d: L = batch): one wave per row, the row held in registers; statistics,
+// running stats and the normalised + PReLU output in ONE launch.
+constexpr int kSmallL = 512;
+constexpr int kSmallPer = kSmallL / 64;
+
+__global__ __launch_bounds__(kNT) void bn_small_fwd_kernel(const float* __restrict__ x, int C, int L,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ alpha, float* running_mean,
+                                                           float* running_var, float momentum, float eps,
+                                                           float* __restrict__ y, float* __restrict__ save_mean,
+                                                           float* __restrict__ save_invstd) {
+  const int c = blockIdx.x * (kNT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const float* row = x + (long)c * L;
+  float v[kSmallPer];
+  double sum = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSmallPer; ++j) {
+    const int i = lane + 64 * j;
+    v[j] = i < L ? row[i] : 0.f;
+    sum += v[j];
+  }
+  const double mean = wave_sum_d(sum) / L;
+  double m2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSmallPer; ++j) {
+    const double d = v[j] - mean;
+    if (lane + 64 * j < L) m2 += d * d;
+  }
+  m2 = wave_sum_d(m2);
+  const float mu = (float)mean, is = (float)(1.0 / sqrt(m2 / L + (double)eps));
+  if (lane == 0) bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
+  const float ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  float* yr = y + (long)c * L;
+#pragma unroll
+  for (int j = 0; j < kSmallPer; ++j) {
+    const int i = lane + 64 * j;
+    if (i < L) {
+      float z = (v[j] - mu) * is * ga + be;
+      if (alpha) z = z > 0.f ? z : al * z;
+      yr[i] = z;
+    }
+  }
+}
+
+// Backward of the short-row form: row sums in double, gx and the parameter gradients in one launch.
+__global__ __launch_bounds__(kNT) void bn_small_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                                                           int C, int L, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ alpha, float* __restrict__ gx,
+                                                           float* __restrict__ ggamma, float* __restrict__ gbeta,
+                                                           float* __restrict__ galpha) {
+  const int c = blockIdx.x * (kNT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  const float* xr = x + (long)c * L;
+  const float* gr = gy + (long)c * L;
+  float xh[kSmallPer], g[kSmallPer];
+  double sg = 0.0, sgx = 0.0, sa = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSmallPer; ++j) {
+    const int i = lane + 64 * j;
+    xh[j] = 0.f;
+    g[j] = 0.f;
+    if (i < L) {
+      xh[j] = (xr[i] - mu) * is;
+      const float gv = gr[i];
+      g[j] = gv;
+      if (alpha) {
+        const float z = xh[j] * ga + be;
+        if (!(z > 0.f)) {
+          g[j] = gv * al;
+          sa += (double)gv * z;
+        }
+      }
+      sg += g[j];
+      sgx += (double)g[j] * xh[j];
+    }
+  }
+  sg = wave_sum_d(sg);
+  sgx = wave_sum_d(sgx);
+  if (alpha) sa = wave_sum_d(sa);
+  if (lane == 0) {
+    gbeta[c] = (float)sg;
+    ggamma[c] = (float)sgx;
+    if (alpha && galpha) galpha[c] = (float)sa;
+  }
+  const float mg = (float)(sg / L), mgx = (float)(sgx / L), k = ga * is;
+  float* gxr = gx + (long)c * L;
+#pragma unroll
+  for (int j = 0; j < kSmallPer; ++j) {
+    const int i = lane + 64 * j;
+    if (i < L) gxr[i] = k * (g[j] - mg - xh[j] * mgx);
   }
 }
 
@@ -118,12 +242,12 @@ __global__ __launch_bounds__(kNT) void bn_act_apply_kernel(const float* __restri
   }
 }
 
-// partial sums of g = gy*prelu'(z), g*xhat and gy*min(z,0)
+// partial sums of g = gy*prelu'(z), g*xhat and gy*min(z,0)  (double, see above)
 __global__ __launch_bounds__(kNT) void bn_act_bwd_partial_kernel(
     const float* __restrict__ gy, const float* __restrict__ x, long L, int S, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
-    const float* __restrict__ alpha, float* __restrict__ part) {
-  __shared__ float sh[4];
+    const float* __restrict__ alpha, double* __restrict__ part) {
+  __shared__ double sh[4];
   const int c = blockIdx.y, s = blockIdx.x;
   const long per = (L + S - 1) / S;
   const long lo = s * per, hi = min(L, lo + per);
@@ -131,7 +255,7 @@ __global__ __launch_bounds__(kNT) void bn_act_bwd_partial_kernel(
   const float al = alpha ? alpha[c] : 1.f;
   const float* xr = x + (long)c * L;
   const float* gr = gy + (long)c * L;
-  float sg = 0.f, sgx = 0.f, sa = 0.f;
+  double sg = 0.0, sgx = 0.0, sa = 0.0;
   for (long i = lo + threadIdx.x; i < hi; i += kNT) {
     const float xh = (xr[i] - mu) * is;
     const float gv = gr[i];
@@ -140,36 +264,36 @@ __global__ __launch_bounds__(kNT) void bn_act_bwd_partial_kernel(
       const float z = xh * ga + be;
       if (!(z > 0.f)) {
         g = gv * al;
-        sa += gv * z;
+        sa += (double)gv * z;
       }
     }
     sg += g;
-    sgx += g * xh;
+    sgx += (double)g * xh;
   }
-  sg = block_sum(sg, sh);
-  sgx = block_sum(sgx, sh);
-  sa = block_sum(sa, sh);
+  sg = block_sum_d(sg, sh);
+  sgx = block_sum_d(sgx, sh);
+  sa = block_sum_d(sa, sh);
   if (threadIdx.x == 0) {
-    float* o = part + ((long)blockIdx.y * S + s) * 3;
+    double* o = part + ((long)blockIdx.y * S + s) * 3;
     o[0] = sg;
     o[1] = sgx;
     o[2] = sa;
   }
 }
 
-__global__ void reduce3_kernel(const float* __restrict__ part, int C, int S, float* o0, float* o1, float* o2) {
+__global__ void reduce3_kernel(const double* __restrict__ part, int C, int S, float* o0, float* o1, float* o2) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const float* p = part + (long)c * S * 3;
-  float a = 0.f, b = 0.f, d = 0.f;
+  const double* p = part + (long)c * S * 3;
+  double a = 0.0, b = 0.0, d = 0.0;
   for (int s = 0; s < S; ++s) {
     a += p[3 * s];
     b += p[3 * s + 1];
     d += p[3 * s + 2];
   }
-  if (o0) o0[c] = a;
-  if (o1) o1[c] = b;
-  if (o2) o2[c] = d;
+  if (o0) o0[c] = (float)a;
+  if (o1) o1[c] = (float)b;
+  if (o2) o2[c] = (float)d;
 }
 
 // gx = gamma*invstd*(g - sum(g)/L - xhat*sum(g*xhat)/L); the partial sums were reduced into
@@ -378,15 +502,20 @@ extern "C" {
 
 const char* ganamd_version(void) { return "ganamd 0.1 gfx950"; }
 
-size_t ganamd_rowreduce_workspace(int C, long L) { return sizeof(float) * 3 * (size_t)C * splits_for(L); }
+size_t ganamd_rowreduce_workspace(int C, long L) { return sizeof(double) * 3 * (size_t)C * splits_for(L); }
 
 int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
                       float* save_mean, float* save_invstd, void* workspace, hipStream_t st) {
   if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || C <= 0 || L <= 0)
     return GANAMD_EINVAL;
+  if (L <= kSmallL) {
+    hipLaunchKernelGGL(bn_small_fwd_kernel, dim3((C + 3) / 4), dim3(kNT), 0, st, x, C, (int)L, gamma, beta, alpha,
+                       running_mean, running_var, momentum, eps, y, save_mean, save_invstd);
+    return ok(hipGetLastError());
+  }
   const int S = splits_for(L);
-  float* part = static_cast<float*>(workspace);
+  double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_partial_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, L, running_mean,
                      running_var, momentum, eps, save_mean, save_invstd);
@@ -400,8 +529,13 @@ int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const floa
                       float* gbeta, float* galpha, void* workspace, hipStream_t st) {
   if (!gy || !x || !gamma || !beta || !save_mean || !save_invstd || !gx || !ggamma || !gbeta || !workspace)
     return GANAMD_EINVAL;
+  if (L <= kSmallL) {
+    hipLaunchKernelGGL(bn_small_bwd_kernel, dim3((C + 3) / 4), dim3(kNT), 0, st, gy, x, C, (int)L, save_mean,
+                       save_invstd, gamma, beta, alpha, gx, ggamma, gbeta, galpha);
+    return ok(hipGetLastError());
+  }
   const int S = splits_for(L);
-  float* part = static_cast<float*>(workspace);
+  double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_act_bwd_partial_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, L, S, save_mean, save_invstd,
                      gamma, beta, alpha, part);
   hipLaunchKernelGGL(reduce3_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, gbeta, ggamma,

@@ -227,10 +227,15 @@ class Conv2dWeightModulate(nn.Module):
         self.k = kernel_size
         assert demodulate, "G13_5 always demodulates"
 
+    _bank_sd = None      # (s, d) handed over by the Generator's style bank for this forward
+
     def forward(self, x, w):
-        s = bn_act(self.to_style[1](self.to_style[0](w)), self.to_style[2], None)   # [Cin, B]
         C, B, H, W = x.shape
         geo = ops.conv_geo(B, C, H, W, self.out_planes, self.k, 1, (self.k - 1) // 2)
+        if self._bank_sd is not None:
+            s, d = self._bank_sd
+            return ops.ModConv.apply(x, s, d, self.weight.weights, geo, self.weight.scale)
+        s = bn_act(self.to_style[1](self.to_style[0](w)), self.to_style[2], None)   # [Cin, B]
         return ops.modconv(x, s, self.weight.weights, geo, self.weight.scale)
 
 
@@ -524,6 +529,9 @@ class GeneratorStart(nn.Module):
         B, zd = z.shape[0], z.shape[1]
         zc = z.reshape(B, zd).t().contiguous()                   # [256, B]
         w = self.mapping_network(zc)
+        hook = self.__dict__.get("_w_hook")
+        if hook is not None:
+            hook(w)
         geo = ops.convT_geo(B, zd, 1, 1, self.convT.out_channels, 4, 1, 0)
         x = ops.conv2d(zc.reshape(zd, B, 1, 1), self.convT.weight, self.convT.bias, geo, 1.0)
         x = bn_act(x, self.bn, self.activation)
@@ -565,6 +573,37 @@ class Generator(nn.Module):
             if isinstance(mod, StyleConv):
                 object.__setattr__(mod, "_hub", hub)
 
+    # ---- style bank (stylebank.py) ----------------------------------------------------------
+    use_bank = True
+
+    def flat_layout(self):
+        """Parameter order for optim.FlatParams: the style bank's parameters first, contiguous."""
+        from .stylebank import bank_param_order
+        first = bank_param_order(self)
+        ids = {id(p) for p in first}
+        return first + [p for p in self.parameters() if id(p) not in ids]
+
+    def _bank(self):
+        if not self.use_bank:
+            return None
+        flat = self.__dict__.get("_flat")
+        if flat is None:
+            return None
+        bank = self.__dict__.get("_style_bank")
+        if bank is None or bank.flat is not flat or not bank.valid():
+            from .stylebank import StyleBank
+            try:
+                bank = StyleBank(self, flat)
+            except RuntimeError:
+                return None
+            self.__dict__["_style_bank"] = bank
+        return bank
+
+    def _run_bank(self, w):
+        s_list, d_list = self.__dict__["_style_bank"](w)
+        for m, s, d in zip(self.__dict__["_style_bank"].mods, s_list, d_list):
+            m.__dict__["_bank_sd"] = (s, d)
+
     def _tracked(self):
         lst = getattr(self, "_nbt", None)
         if lst is None or (lst and lst[0].device != self.block0.bn.weight.device):
@@ -575,11 +614,18 @@ class Generator(nn.Module):
     def forward(self, x):
         if not self.training:
             raise NotImplementedError("G13_5 is only ever run in train mode (batch statistics)")
-        h, w, rgb = self.block0(x)
-        h, rgb = self.block1(h, w, rgb)
-        h, rgb = self.block2(h, w, rgb)
-        h, rgb = self.block3(h, w, rgb)
-        h, rgb = self.block4(h, w, rgb)
+        bank = self._bank()
+        self.block0.__dict__["_w_hook"] = self._run_bank if bank is not None else None
+        try:
+            h, w, rgb = self.block0(x)
+            h, rgb = self.block1(h, w, rgb)
+            h, rgb = self.block2(h, w, rgb)
+            h, rgb = self.block3(h, w, rgb)
+            h, rgb = self.block4(h, w, rgb)
+        finally:
+            if bank is not None:
+                for m in bank.mods:
+                    m.__dict__["_bank_sd"] = None
         with torch.no_grad():
             torch._foreach_add_(self._tracked(), 1)
         return ops.cnhw_to_nchw(rgb)

@@ -29,7 +29,9 @@ class FlatParams:
         for mname, mod in module.named_modules():
             for pname, p in mod.named_parameters(recurse=False):
                 owners[id(p)] = (type(mod).__name__, pname)
-        params = list(module.parameters())
+        layout = getattr(module, "flat_layout", None)
+        params = list(layout()) if layout is not None else list(module.parameters())
+        assert len({id(p) for p in params}) == len(list(module.parameters())), "flat_layout must permute parameters()"
         train = [p for p in params if p.requires_grad and not _never_gets_grad(*owners[id(p)])]
         tids = {id(p) for p in train}
         rest = [p for p in params if id(p) not in tids]
@@ -49,6 +51,7 @@ class FlatParams:
             if off < n_train:
                 p.grad = self.grad[off:off + n].view_as(p)
             off += n
+        module.__dict__["_flat"] = self      # lets the module find its flat buffers (style bank)
 
     def zero_grad(self):
         self.grad.zero_()

@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--mode", choices=["eager", "graph"], default="graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-bank", action="store_true", help="per-module style MLPs (A/B against the style bank)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
     return ap.parse_args()
 
@@ -104,6 +105,7 @@ def main():
 
     torch.manual_seed(1234)                         # identical initial weights on every rank
     G = gan_amd.Generator(256).to(dev)
+    G.use_bank = not args.no_bank
     D = gan_amd.Discriminator().to(dev)
     torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
     tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev))

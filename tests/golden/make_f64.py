@@ -50,6 +50,59 @@ def grad_rows(P, names):
                        for n in names])
 
 
+def g_out_spread(trials=12):
+    """fp32 rounding spread of the G13_5 forward at B=4: the oracle in fp32 with every weight
+    perturbed by ~1 ulp (relative N(0, 6e-8)), distance to float64 truth per trial.  One fp32
+    evaluation order is one draw from this distribution (the reference's own error is one
+    such draw), so the GPU bar is set on the distribution, not on that single draw."""
+    pl = plan()
+    fx = fixture("g_fwd_b4.npz")
+    truth = fixture("f64_truth.npz")["g_out"]
+    errs = []
+    for t in range(1, trials + 1):
+        GP = om.params_from_plan(pl["g_params"], pl["g_seed"])
+        g = torch.Generator().manual_seed(t)
+        with torch.no_grad():
+            for v in GP.t.values():
+                v.mul_(1 + 6e-8 * torch.randn(v.shape, generator=g))
+            out = om.generator(GP, torch.from_numpy(fx["z"]), om.Draw(101).randn)
+        errs.append(rel_err(out.numpy(), truth))
+        print("spread trial", t, errs[-1], flush=True)
+    return np.asarray(errs)
+
+
+def step_spread(trials=6):
+    """Same idea for the training steps: gradient statistics (tests/_util.grad_norm_stats) of the
+    fp32 oracle with ~1-ulp perturbed weights against float64 truth, per trial."""
+    pl = plan()
+    truth = fixture("f64_truth.npz")
+    dnames = [n for n, _, _ in pl["d_params"]]
+    gnames = [n for n, _, _ in pl["g_params"]]
+    res = {f"d{B}_fp32_spread": [] for B in (4, 8)}
+    res["g_fp32_spread"] = []
+    for t in range(1, trials + 1):
+        for B, img_seed, rng_seed in ((4, 300, 301), (8, 310, 311), (4, None, 401)):
+            GP = om.params_from_plan(pl["g_params"], pl["g_seed"])
+            DP = om.params_from_plan(pl["d_params"], pl["d_seed"])
+            g = torch.Generator().manual_seed(t)
+            with torch.no_grad():
+                for v in list(GP.t.values()) + list(DP.t.values()):
+                    v.mul_(1 + 6e-8 * torch.randn(v.shape, generator=g))
+            tr = om.WGANGP(GP, DP)
+            if img_seed is None:
+                tr.generator_trainstep(4, om.Draw(rng_seed))
+                rows = grad_rows(GP, gnames)
+                key, tkey = "g_fp32_spread", "g_grads"
+            else:
+                images = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed))
+                tr.discriminator_trainstep(images, B, om.Draw(rng_seed))
+                rows = grad_rows(DP, dnames)
+                key, tkey = f"d{B}_fp32_spread", f"d{B}_grads"
+            res[key].append(grad_norm_stats(rows, truth[tkey]))
+            print("step spread", t, key, res[key][-1], flush=True)
+    return {k: np.asarray(v) for k, v in res.items()}
+
+
 def main():
     torch.set_num_threads(os.cpu_count() or 8)
     om._SMOOTH = om._SMOOTH.to(DT)
@@ -92,7 +145,21 @@ def main():
     out["ref_g_stats"] = np.asarray(grad_norm_stats(fx["grads"], rows))
     print("g step", time.time() - t0, out["ref_g_stats"], flush=True)
     np.savez_compressed(os.path.join(HERE, "f64_truth.npz"), **out)
+    out["g_out_fp32_spread"] = g_out_spread()
+    np.savez_compressed(os.path.join(HERE, "f64_truth.npz"), **out)
+    out.update(step_spread())
+    np.savez_compressed(os.path.join(HERE, "f64_truth.npz"), **out)
 
 
 if __name__ == "__main__":
-    main()
+    if "--spread-only" in sys.argv:     # add/refresh only the fp32 spread entry
+        torch.set_num_threads(os.cpu_count() or 8)
+        path = os.path.join(HERE, "f64_truth.npz")
+        cur = dict(np.load(path))
+        if "--steps" in sys.argv:
+            cur.update(step_spread())
+        else:
+            cur["g_out_fp32_spread"] = g_out_spread()
+        np.savez_compressed(path, **cur)
+    else:
+        main()

@@ -25,9 +25,15 @@ def truth():
     return fixture("f64_truth.npz")
 
 
-def check_vs_truth(rows, truth_rows, ref_stats):
+def check_vs_truth(rows, truth_rows, ref_stats, spread=None):
+    """Gradient statistics vs float64 truth within 2x what fp32 itself reaches: the reference's
+    own run (ref_stats) and, when given, the largest of the ~1-ulp-perturbed fp32 oracle runs
+    (tests/golden/make_f64.py step_spread) -- one fp32 summation order is one draw."""
     got = grad_norm_stats(rows, truth_rows)
-    bars = [2 * r + 1e-5 for r in ref_stats]
+    worst = np.asarray(ref_stats, dtype=np.float64)
+    if spread is not None:
+        worst = np.maximum(worst, np.asarray(spread).max(axis=0))
+    bars = [2 * r + 1e-5 for r in worst]
     assert all(g <= b for g, b in zip(got, bars)), ("gpu-vs-f64", got, "bars", bars)
     return got
 
@@ -50,18 +56,28 @@ def make_D(gan, P):
     return D.to(DEV)
 
 
-def test_g_forward_b4(gan, P, truth):
+@pytest.mark.parametrize("bank", [False, True])
+def test_g_forward_b4(gan, P, truth, bank):
+    """bank=True: the 519 style MLPs / demodulations run as the style bank (stylebank.py)."""
+    from gan_amd.optim import FlatParams
     fx = fixture("g_fwd_b4.npz")
     G = make_G(gan, P)
+    if bank:
+        FlatParams(G)
     rng = gan.ReplayRNG(101, DEV)
     G.noise_hub.source = rng.noise
     with torch.no_grad():
         out = G(torch.from_numpy(fx["z"]).to(DEV))
     torch.cuda.synchronize()
+    assert (G.__dict__.get("_style_bank") is not None) == bank
     assert tuple(out.shape) == (4, 3, 64, 64)
     err = rel_err(out.cpu().numpy(), fx["out"])
     assert err < 1e-3, err
-    assert rel_err(out.cpu().numpy(), truth["g_out"]) < 2 * float(truth["ref_g_out_err"])
+    # fp32 rounding of this forward is amplified by BatchNorm1d over B=4: with ~1-ulp weight
+    # perturbations the CPU fp32 oracle lands 1.9e-4..4.5e-4 from float64 truth (the reference's
+    # own run: 2.0e-4), and the same torch ops executed on MI355X 4.2e-4..8.3e-4
+    # (tools/g_precision.py).  Bar: within 2x the largest CPU fp32 draw.
+    assert rel_err(out.cpu().numpy(), truth["g_out"]) < 2 * float(truth["g_out_fp32_spread"].max())
     assert [list(s) for _, s in rng.log] == P["g_noise_shapes_b4"]
     buf = np.asarray([[float(b.double().sum()), float(b.double().norm())] for _, b in G.named_buffers()])
     assert rel_err(buf, fx["buffers"]) < 1e-4
@@ -103,7 +119,7 @@ def test_d_step(gan, P, truth, B, img_seed, rng_seed):
     rows = _rows(D, names)
     has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
     assert (has == fx["has_grad"]).all()
-    check_vs_truth(rows, truth[f"d{B}_grads"], truth[f"ref_d{B}_stats"])
+    check_vs_truth(rows, truth[f"d{B}_grads"], truth[f"ref_d{B}_stats"], truth[f"d{B}_fp32_spread"])
     assert rel_err(losses, truth[f"d{B}_losses"]) <= 2 * float(truth[f"ref_d{B}_loss_err"]) + 1e-6
     params = dict(D.named_parameters())
     dl = np.asarray([tensor_summary((params[n].detach() - before[n]) / 4e-4)[1] for n in names])
@@ -121,7 +137,36 @@ def test_g_step(gan, P, truth):
     rows = _rows(G, names)
     has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
     assert (has == fx["has_grad"]).all()
-    check_vs_truth(rows, truth["g_grads"], truth["ref_g_stats"])
+    check_vs_truth(rows, truth["g_grads"], truth["ref_g_stats"], truth["g_fp32_spread"])
     # the critic was frozen only for the backward (its weight gradient is dead work there)
     assert all(p.requires_grad for n, p in D.named_parameters() if not n.endswith("kernel"))
     assert float(tr.optimizer_D.flat.grad.abs().sum()) == 0.0
+
+
+def test_style_bank_matches_modules(gan, P):
+    """Style bank vs the per-module path on the same weights and noise: outputs, BN running
+    statistics, and every parameter gradient (norm-based statistics of tests/_util.py, which skip
+    the structurally-zero gradients of biases that feed a BatchNorm).  The two paths differ only in
+    fp32 summation order; the G backward amplifies that (see test_g_step's bars)."""
+    from gan_amd.optim import FlatParams
+    z = torch.randn(8, 256, 1, 1, generator=torch.Generator().manual_seed(5)).to(DEV)
+    res = []
+    for use in (False, True):
+        G = make_G(gan, P)
+        FlatParams(G)
+        G.use_bank = use
+        G.noise_hub.source = gan.ReplayRNG(7, DEV).noise
+        out = G(z)
+        r = torch.randn(out.shape, generator=torch.Generator().manual_seed(3)).to(DEV)
+        (out * r).sum().backward()
+        torch.cuda.synchronize()
+        assert (G.__dict__.get("_style_bank") is not None) == use
+        bufs = torch.cat([b.detach().double().reshape(-1) for _, b in G.named_buffers()]).cpu()
+        rows = [tensor_summary(p.grad) for _, p in G.named_parameters() if p.grad is not None]
+        res.append((out.detach().double().cpu(), bufs, np.asarray(rows)))
+        del G
+    (o0, b0, r0), (o1, b1, r1) = res
+    assert rel_err(o1.numpy(), o0.numpy()) < 1e-4
+    assert rel_err(b1.numpy(), b0.numpy()) < 1e-5
+    med, p99, mx, vec = grad_norm_stats(r1, r0)
+    assert med < 2e-3 and vec < 2e-3, (med, p99, mx, vec)

@@ -291,3 +291,59 @@ def test_adamw_matches_torch():
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         assert torch.allclose(p1, p2, rtol=1e-5, atol=1e-6)
     assert int(o2.step_count.item()) == 5
+
+
+@pytest.mark.parametrize("a_t,b_t,sq", [(0, 0, 0), (1, 0, 0), (0, 1, 1), (1, 1, 0), (0, 0, 1)])
+def test_grouped_gemm(a_t, b_t, sq):
+    """ganamd_grouped_gemm vs float64 torch over ragged groups, every epilogue, multi-tile groups."""
+    from gan_amd import _lib
+    from gan_amd.stylebank import _tiles, grouped_gemm
+    g = torch.Generator().manual_seed(11 + 2 * a_t + b_t)
+    shapes = [(70, 33, 5), (64, 64, 64), (1, 17, 130), (130, 1, 3), (96, 80, 257)]   # rows, cols, K
+    epis = [_lib.EPI_STORE, _lib.EPI_BIAS, _lib.EPI_SCALE, _lib.EPI_ACCUM, _lib.EPI_DEMOD]
+    A, Bm, Cinit, want, tiles = [], [], [], [], []
+    ao = bo = co = 0
+    bias = torch.randn(512, generator=g, dtype=torch.float64)
+    for gi, ((R, N, K), epi) in enumerate(zip(shapes, epis)):
+        a = torch.randn(R, K, generator=g, dtype=torch.float64)
+        b = torch.randn(K, N, generator=g, dtype=torch.float64)
+        if epi == _lib.EPI_DEMOD:
+            a = a.abs()
+        c0 = torch.randn(R, N, generator=g, dtype=torch.float64)
+        scale = 0.37 + gi
+        acc = a @ (b * b if sq else b)
+        if epi == _lib.EPI_STORE:
+            w = acc
+        elif epi == _lib.EPI_BIAS:
+            w = scale * acc + bias[gi:gi + R, None]
+        elif epi == _lib.EPI_SCALE:
+            w = scale * acc
+        elif epi == _lib.EPI_ACCUM:
+            w = c0 + scale * acc
+        else:
+            w = 1 / torch.sqrt(scale * scale * (a @ (b * b)) + 1e-8) if sq else None
+        if w is None:   # DEMOD needs a non-negative accumulator: use |a| @ b^2 via squared B
+            continue
+        A.append((a.t() if a_t else a).contiguous().reshape(-1))
+        Bm.append((b.t() if b_t else b).contiguous().reshape(-1))
+        Cinit.append(c0.reshape(-1))
+        want.append(w.reshape(-1))
+        lda = R if a_t else K
+        ldb = K if b_t else N
+        for r0 in range(0, R, 64):
+            for n0 in range(0, N, 64):
+                a_off = ao + (r0 if a_t else r0 * K)
+                b_off = bo + (n0 * K if b_t else n0)
+                tiles.append([a_off, lda, b_off, ldb, co + r0 * N + n0, N, min(64, R - r0), min(64, N - n0), K, epi,
+                              gi + r0, scale])
+        ao += R * K
+        bo += K * N
+        co += R * N
+    dev = "cuda"
+    T = torch.from_numpy(_tiles(tiles)).to(dev)
+    C = torch.cat(Cinit).float().to(dev)
+    grouped_gemm(torch.cat(A).float().to(dev), torch.cat(Bm).float().to(dev), C, T, a_trans=bool(a_t),
+                 b_trans=bool(b_t), b_square=bool(sq), bias=bias.float().to(dev))
+    got = C.double().cpu()
+    ref = torch.cat(want)
+    assert rel(got, ref) < 1e-5
