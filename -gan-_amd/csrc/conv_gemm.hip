@@ -463,11 +463,11 @@ int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96
 
 Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_splits) {
   int splits = 1;
-  // a GEMM whose whole K loop is short is launch-bound: one more launch for the reduce costs
-  // more than the idle CUs (the 519 per-conv style MLPs are this case)
+  // split K while the grid is short of `target` workgroups, keeping >= 4 K-steps per split; a GEMM
+  // whose whole loop is tiny (tiles * K-steps < 256) is launch-bound and is left alone
   const long work = (long)tiles * kt_total;
-  if (tiles < target && kt_total >= 16 && work >= 4096)
-    splits = std::min((target + tiles - 1) / tiles, std::max(1, kt_total / 8));
+  if (tiles < target && kt_total >= 8 && work >= 256)
+    splits = std::min((target + tiles - 1) / tiles, std::max(1, kt_total / 4));
   splits = std::min(splits, max_splits);
   const int per = (kt_total + splits - 1) / splits;
   splits = (kt_total + per - 1) / per;
