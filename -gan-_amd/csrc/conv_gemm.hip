@@ -102,9 +102,10 @@ __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int k
 }
 
 struct ConvArgs {
-  const float* w;      // A(m, t, c) = w[m*sm + c*sc + t*st]
+  const float* w;      // packed A[Mpad][T][Ckp] (see pack_a_kernel); before packing A(m,t,c) = w[m*sm + c*sc + t*st]
   int sm, sc, st, w_bytes;
   int M, Ck, T;        // GEMM rows, channels per tap, taps
+  int Ckp;             // Ck rounded up to whole K-steps
   Gather g;
   float* y;            // Y[m][n]
   const float* bias;   // [M] or null
@@ -180,31 +181,59 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
 // ------------------------------------------------------------------------------------------
 // forward / dgrad / transposed: K = (tap, channel), N = output pixels
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, int KS>
+// The A operand (weights) is first packed into GEMM order A[m][t][c] (m < Mpad, c < Ckp, zero
+// padded to the tile grid and to whole K-steps) so that every K-step of a row is 64 contiguous
+// bytes: one 16-byte buffer load per 4 k-values, no bounds tests.  The B operand is the
+// im2col/transposed gather; a thread owns one pixel n and KPT consecutive channels of the K-step.
+__global__ void pack_a_kernel(const float* __restrict__ w, int sm, int sc, int st, int M, int Ck, int T, int Mpad,
+                              int Ckp, float* __restrict__ out) {
+  const long total = (long)Mpad * T * Ckp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Ckp);
+    const long r = i / Ckp;
+    const int t = (int)(r % T);
+    const int m = (int)(r / T);
+    out[i] = (m < M && c < Ck) ? w[(long)m * sm + (long)c * sc + (long)t * st] : 0.f;
+  }
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
 __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
-  constexpr int LD = KS + 2;
   using C = TileCfg<BM, BN, WGM, WGN>;
-  constexpr int EA = KS * BM / kThreads;
-  constexpr int EB = KS * BN / kThreads;
-  static_assert(kThreads % BN == 0, "B mapping: n fixed per thread");
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LD];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LD];
+  constexpr int A4 = BM * BK / 4;                      // 16-byte slots of the A tile
+  constexpr int EA = (A4 + kThreads - 1) / kThreads;   // slots per thread
+  constexpr int KPT = BK * BN / kThreads;              // B k-values per thread
+  static_assert(KPT % 2 == 0 && BK % KPT == 0, "B mapping");
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int nct = (p.Ck + KS - 1) / KS;
+  const int nct = p.Ckp / BK;
   const int kt_total = nct * p.T;
   const int kt0 = blockIdx.z * p.kt_per_split;
   const int kt1 = min(kt_total, kt0 + p.kt_per_split);
   if (kt0 >= kt1) return;
 
-  // A mapping: k fixed per thread, m strided.  B mapping: n fixed per thread, k strided.
-  const int a_k = tid % KS, a_m = tid / KS;
-  constexpr int A_MSTEP = kThreads / KS;
-  const int b_n = tid % BN, b_k = tid / BN;
-  constexpr int B_KSTEP = kThreads / BN;
+  // A slots: row m = slot/4, k = 4*(slot%4) (+ kt*BK): contiguous along the packed row
+  const int Krow = p.T * p.Ckp;
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  int a_off[EA];
+#pragma unroll
+  for (int e = 0; e < EA; ++e) {
+    const int slot = tid + e * kThreads;
+    a_off[e] = 4 * ((m0 + (slot >> 2)) * Krow + 4 * (slot & 3));
+  }
 
+  // B: pixel n = n0 + tid % BN, channels c0 + kg*KPT .. +KPT-1 of the K-step
+  const int b_n = tid % BN, b_kg = tid / BN;
   const Gather& g = p.g;
   const int gn = n0 + b_n;
   const bool n_ok = gn < p.N;
@@ -215,44 +244,54 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     oh = rr / g.OW;
     ow = rr - oh * g.OW;
   }
-  const int cstride = g.B * g.H * g.W;
+  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
   const int img = bb * g.H * g.W;
-  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
   const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
   const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
 
-  float ra[EA], rb[EB], rs[EB];
-  int cur_t = -1, sp = -1;
+  f32x4 ra[EA];
+  float rb[KPT], rs[KPT];
+  // (t, cc): tap and channel chunk of the next K-step to load
+  int t = kt0 / nct, cc = kt0 - (kt0 / nct) * nct;
+  auto tap = [&](int tt) {
+    const int kh = tt / g.KW;
+    return n_ok ? tap_offset<MODE>(g, oh, ow, kh, tt - kh * g.KW) : -1;
+  };
+  int sp = tap(t);
 
   auto gload = [&](int kt) {
-    const int t = kt / nct;
-    const int c0 = (kt - t * nct) * KS;
-    if (t != cur_t) {
-      cur_t = t;
-      const int kh = t / g.KW;
-      sp = n_ok ? tap_offset<MODE>(g, oh, ow, kh, t - kh * g.KW) : -1;
-    }
-    const int ca = c0 + a_k;
-    const bool caok = ca < p.Ck;
-    const int abase = ca * p.sc + t * p.st;
 #pragma unroll
-    for (int e = 0; e < EA; ++e) {
-      const int m = m0 + a_m + e * A_MSTEP;
-      ra[e] = bload(rw, (caok && m < p.M) ? 4 * (abase + m * p.sm) : kOOB);
-    }
+    for (int e = 0; e < EA; ++e)
+      if (tid + e * kThreads < A4) ra[e] = bload4(rw, a_off[e] + kt * (BK * 4));
+    const int c = cc * BK + b_kg * KPT;
+    // channels past the source's end fall outside the buffer: the hardware returns 0
+    const unsigned base = sp >= 0 ? 4u * (unsigned)(img + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
+    const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + bb) : (unsigned)kOOB;
 #pragma unroll
-    for (int e = 0; e < EB; ++e) {
-      const int c = c0 + b_k + e * B_KSTEP;
-      const bool ok = sp >= 0 && c < p.Ck;
-      rb[e] = bload(rx, ok ? 4 * (img + c * cstride + sp) : kOOB);
-      if (BSCALE) rs[e] = bload(rsc, ok ? 4 * (c * g.B + bb) : kOOB);
+    for (int e = 0; e < KPT; ++e) {
+      rb[e] = bload(rx, (int)(base + (unsigned)e * cs4));
+      if (BSCALE) rs[e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
+    }
+    if (++cc == nct) {
+      cc = 0;
+      if (++t < p.T) sp = tap(t);
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][(a_m + e * A_MSTEP) * LD + a_k] = ra[e];
+    for (int e = 0; e < EA; ++e) {
+      const int slot = tid + e * kThreads;
+      if (slot < A4) {
+        float* d = &As[buf][(slot >> 2) * LDK + 4 * (slot & 3)];
+        *reinterpret_cast<f32x2*>(d) = f32x2{ra[e][0], ra[e][1]};
+        *reinterpret_cast<f32x2*>(d + 2) = f32x2{ra[e][2], ra[e][3]};
+      }
+    }
+    float* d = &Bs[buf][b_n * LDK + b_kg * KPT];
 #pragma unroll
-    for (int e = 0; e < EB; ++e) Bs[buf][b_n * LD + b_k + e * B_KSTEP] = BSCALE ? rb[e] * rs[e] : rb[e];
+    for (int e = 0; e < KPT; e += 2)
+      *reinterpret_cast<f32x2*>(d + e) =
+          BSCALE ? f32x2{rb[e] * rs[e], rb[e + 1] * rs[e + 1]} : f32x2{rb[e], rb[e + 1]};
   };
 
   f32x16 acc[C::TM][C::TN];
@@ -265,8 +304,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-#pragma unroll
-    for (int k0 = 0; k0 < KS; k0 += 16) mfma_tile<C, LD>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
+    mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -435,10 +473,6 @@ int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
-int conv_ks() {
-  static const int v = env_int("GANAMD_CONV_KS", 16);
-  return v;
-}
 int conv_block_target() {
   static const int v = env_int("GANAMD_CONV_BLOCKS", 1024);
   return v;
@@ -454,7 +488,7 @@ int wgrad_block_target() {
 // kernel folds the slabs.  The plan is a pure function of the geometry so the workspace query
 // and the launch agree.
 struct Plan {
-  int bm, bn, splits, kt_per_split, ks = 16;
+  int bm, bn, splits, kt_per_split;
 };
 
 int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
@@ -475,11 +509,16 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_spl
 }
 
 Plan conv_plan(int M, int N, int Ck, int T) {
-  const int bm = conv_bm(M), bn = conv_bn(bm), ks = conv_ks();
+  const int bm = conv_bm(M), bn = conv_bn(bm);
   const int tiles = ((N + bn - 1) / bn) * ((M + bm - 1) / bm);
-  Plan pl = split_plan(bm, bn, tiles, ((Ck + ks - 1) / ks) * T, conv_block_target(), 16);
-  pl.ks = ks;
-  return pl;
+  return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, conv_block_target(), 16);
+}
+
+// bytes of the packed A operand of a conv GEMM (rows padded to the tile, K to whole K-steps)
+size_t pack_bytes(int M, int Ck, int T) {
+  const Plan pl = conv_plan(M, 1, Ck, T);   // bm depends on M only
+  const size_t mpad = (size_t)((M + pl.bm - 1) / pl.bm) * pl.bm;
+  return sizeof(float) * mpad * T * (size_t)((Ck + BK - 1) / BK * BK);
 }
 
 Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
@@ -522,12 +561,8 @@ hipError_t launch_conv(ConvArgs p, const Plan& pl, float* slab, hipStream_t st) 
   const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
   p.kt_per_split = pl.kt_per_split;
   p.slab = pl.splits > 1 ? slab : nullptr;
-  if (pl.ks == 32)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, 32>), dim3(gx, gy, pl.splits), dim3(kThreads),
-                       0, st, p);
-  else
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, 16>), dim3(gx, gy, pl.splits), dim3(kThreads),
-                       0, st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3(gx, gy, pl.splits), dim3(kThreads), 0,
+                     st, p);
   if (pl.splits > 1)
     hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.N)), dim3(256), 0, st, slab, pl.splits,
                        p.M, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.y);
@@ -544,9 +579,16 @@ hipError_t dispatch_conv_tile(const ConvArgs& p, const Plan& pl, float* slab, hi
   }
 }
 
-hipError_t dispatch_conv(const ConvArgs& p, float* slab, hipStream_t st) {
+// p.w/sm/sc/st describe the weights as stored; `packed` (pack_bytes) receives the GEMM-order copy.
+hipError_t dispatch_conv(ConvArgs p, float* packed, float* slab, hipStream_t st) {
   const Plan pl = conv_plan(p.M, p.N, p.Ck, p.T);
-  if (pl.splits > 1 && !slab) return hipErrorInvalidValue;
+  if ((pl.splits > 1 && !slab) || !packed) return hipErrorInvalidValue;
+  const int mpad = (p.M + pl.bm - 1) / pl.bm * pl.bm;
+  p.Ckp = (p.Ck + BK - 1) / BK * BK;
+  hipLaunchKernelGGL(pack_a_kernel, dim3(grid1d((long)mpad * p.T * p.Ckp)), dim3(256), 0, st, p.w, p.sm, p.sc, p.st,
+                     p.M, p.Ck, p.T, mpad, p.Ckp, packed);
+  p.w = packed;
+  p.w_bytes = 4 * mpad * p.T * p.Ckp;
   const bool s = p.g.scale != nullptr;
   switch (p.g.mode) {
     case kZero:
@@ -636,11 +678,12 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   if (op == GANAMD_CONV_FWD) {
     fwd_gemm(d, &M, &N, &Ck, &T);
     const Plan pl = conv_plan(M, N, Ck, T);
-    *bytes = pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0;
+    *bytes = align256(pack_bytes(M, Ck, T)) + (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
     const Plan pl = conv_plan(M, N, Ck, T);
-    *bytes = align256(dgrad_pad_bytes(d)) + (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
+    *bytes = align256(pack_bytes(M, Ck, T)) + align256(dgrad_pad_bytes(d)) +
+             (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
     T = d->KH * d->KW;
@@ -658,7 +701,7 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
                     hipStream_t stream) {
-  if (!desc_ok(d) || !x || !w || !y) return GANAMD_EINVAL;
+  if (!desc_ok(d) || !x || !w || !y || !workspace) return GANAMD_EINVAL;
   ConvArgs p{};
   int M, N, Ck, T;
   fwd_gemm(d, &M, &N, &Ck, &T);
@@ -683,12 +726,14 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
   p.alpha = alpha;
   p.N = N;
   p.ohw = d->OH * d->OW;
-  return dispatch_conv(p, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  char* ws = static_cast<char*>(workspace);
+  float* slab = reinterpret_cast<float*>(ws + align256(pack_bytes(M, Ck, T)));
+  return dispatch_conv(p, reinterpret_cast<float*>(ws), slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale, float alpha,
                       float* gx, void* workspace, hipStream_t stream) {
-  if (!desc_ok(d) || !gy || !w || !gx) return GANAMD_EINVAL;
+  if (!desc_ok(d) || !gy || !w || !gx || !workspace) return GANAMD_EINVAL;
   int M, N, Ck, T;
   dgrad_gemm(d, &M, &N, &Ck, &T);
   ConvArgs p{};
@@ -704,7 +749,9 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   p.N = N;
   const size_t pad_bytes = dgrad_pad_bytes(d);
   char* ws = static_cast<char*>(workspace);
-  float* slab = ws ? reinterpret_cast<float*>(ws + align256(pad_bytes)) : nullptr;
+  float* packed = reinterpret_cast<float*>(ws);
+  ws += align256(pack_bytes(M, Ck, T));
+  float* slab = reinterpret_cast<float*>(ws + align256(pad_bytes));
   if (d->transposed) {
     // dX of ConvT = plain zero-padded conv of gy with W viewed [Cin][Cout][KH][KW]
     p.sm = d->Cout * T;
@@ -712,18 +759,17 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, kZero};
     p.y = gx;
     p.ohw = d->H * d->W;
-    return dispatch_conv(p, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+    return dispatch_conv(p, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   // dX of conv = transposed gather of gy into the padded input frame, then fold the pad
   p.sm = T;
   p.sc = d->Cin * T;
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
-  if (pad_bytes && !ws) return GANAMD_EINVAL;
   float* out = pad_bytes ? reinterpret_cast<float*>(ws) : gx;
   p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
   p.y = out;
   p.ohw = Hp * Wp;
-  if (dispatch_conv(p, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+  if (dispatch_conv(p, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
   if (pad_bytes) {
     const long planes = (long)d->Cin * d->B;
     hipLaunchKernelGGL(fold_pad_kernel, dim3(grid1d(planes * d->H * d->W)), dim3(256), 0, stream, out, gx, planes,
