@@ -63,6 +63,13 @@ __device__ __forceinline__ float bload(rsrc_t r, int byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, int byte_off) {
+  asm("" : "+v"(byte_off));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
 // Gather of a CNHW source tensor as a GEMM operand indexed by (tap, channel, n).
 struct Gather {
   const float* src;
@@ -195,12 +202,6 @@ __global__ void pack_a_kernel(const float* __restrict__ w, int sm, int sc, int s
     const int m = (int)(r / T);
     out[i] = (m < M && c < Ck) ? w[(long)m * sm + (long)c * sc + (long)t * st] : 0.f;
   }
-}
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 bload4(rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
 
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
@@ -341,7 +342,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
 __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
-  constexpr int EA = BKW * BM / kThreads;
+  constexpr int A4 = BM * BKW / 4;                     // 16-byte slots of the A tile (4 pixels of a row)
+  constexpr int EA = (A4 + kThreads - 1) / kThreads;
   constexpr int EB = BKW * BN / kThreads;
   constexpr int RSTEP = kThreads / BKW;
   __shared__ __attribute__((aligned(16))) float As[2][BM * LDKW];
@@ -359,45 +361,94 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
 
   const Gather& g = p.g;
   const int kh = t / g.KW, kw = t - kh * g.KW;
-  const int cstride = g.B * g.H * g.W;
-  const int tk = tid % BKW;   // k (pixel) fixed per thread for both operands
-  const int tr = tid / BKW;   // row (m or j) base
+  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
+  const int tk = tid % BKW;   // B: pixel fixed per thread
+  const int tr = tid / BKW;   // B: channel base
 
   const rsrc_t ra_r = make_rsrc(p.a, p.a_bytes);
   const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
   const rsrc_t rsa_r = make_rsrc(SCALED ? p.ascale : p.a, SCALED ? 4 * p.M * g.B : 0);
   const rsrc_t rsb_r = make_rsrc(SCALED ? g.scale : g.src, SCALED ? g.scale_bytes() : 0);
+  // 16-byte A loads need 16-byte aligned rows; a quad of pixels shares its sample when ohw % 4 == 0
+  const bool vec_ok = (p.lda & 3) == 0;
+  const bool quad_b = (p.ohw & 3) == 0;
 
-  float ra[EA], rb[EB], rsa[EA], rsb[EB];
+  f32x4 ra[EA], rsa[EA];
+  float rb[EB], rsb[EB];
+  // pixel of this thread's B column for the next K-step, advanced by BKW pixels per step
+  const int d_b = BKW / p.ohw, d_rem = BKW - d_b * p.ohw, d_oh = d_rem / g.OW, d_ow = d_rem - d_oh * g.OW;
+  int pb, poh, pow_;
+  {
+    const int n = kt0 * BKW + tk;
+    pb = n / p.ohw;
+    const int rr = n - pb * p.ohw;
+    poh = rr / g.OW;
+    pow_ = rr - poh * g.OW;
+  }
   auto gload = [&](int kt) {
-    const int n = kt * BKW + tk;
-    const bool nok = n < p.K;
-    int b = 0, sp = -1;
-    if (nok) {
-      b = n / p.ohw;
-      const int rr = n - b * p.ohw;
-      const int oh = rr / g.OW;
-      sp = tap_offset<MODE>(g, oh, rr - oh * g.OW, kh, kw);
-    }
+    // ---- A: rows m of gy (or x), 4 consecutive pixels per slot
+    const bool full = vec_ok && (kt + 1) * BKW <= p.K;
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
-      const int m = m0 + tr + e * RSTEP;
-      const bool ok = nok && m < p.M;
-      ra[e] = bload(ra_r, ok ? 4 * (m * p.lda + n) : kOOB);
-      if (SCALED) rsa[e] = bload(rsa_r, ok ? 4 * (m * g.B + b) : kOOB);
+      const int slot = tid + e * kThreads;
+      if (slot < A4) {
+        const int m = m0 + (slot >> 3), n = kt * BKW + 4 * (slot & 7);
+        const bool mok = m < p.M;
+        if (full) {
+          ra[e] = bload4(ra_r, mok ? 4 * (m * p.lda + n) : kOOB);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ra[e][i] = bload(ra_r, (mok && n + i < p.K) ? 4 * (m * p.lda + n + i) : kOOB);
+        }
+        if (SCALED) {
+          if (quad_b) {
+            const float sv = bload(rsa_r, mok ? 4 * (m * g.B + min(n, p.K - 1) / p.ohw) : kOOB);
+            rsa[e] = f32x4{sv, sv, sv, sv};
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              rsa[e][i] = bload(rsa_r, (mok && n + i < p.K) ? 4 * (m * g.B + (n + i) / p.ohw) : kOOB);
+          }
+        }
+      }
     }
-    const int img = b * g.H * g.W;
+    // ---- B: the gathered source at tap t, pixel n = kt*BKW + tk (tracked incrementally as
+    // (pb, poh, pow)), channels j0 + tr + e*RSTEP
+    const int n = kt * BKW + tk;
+    const int b = pb;
+    const int sp = n < p.K ? tap_offset<MODE>(g, poh, pow_, kh, kw) : -1;
+    pow_ += d_ow;
+    if (pow_ >= g.OW) {
+      pow_ -= g.OW;
+      ++poh;
+    }
+    poh += d_oh;
+    if (poh >= g.OH) {
+      poh -= g.OH;
+      ++pb;
+    }
+    pb += d_b;
+    // channels past the source's end fall outside the buffer: the hardware returns 0
+    const unsigned base = sp >= 0 ? 4u * (unsigned)(b * g.H * g.W + sp) + (unsigned)(j0 + tr) * cs4 : (unsigned)kOOB;
+    const unsigned sbase = sp >= 0 ? 4u * (unsigned)((j0 + tr) * g.B + b) : (unsigned)kOOB;
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
-      const int jj = j0 + tr + e * RSTEP;
-      const bool ok = sp >= 0 && jj < p.J;
-      rb[e] = bload(rx, ok ? 4 * (img + jj * cstride + sp) : kOOB);
-      if (SCALED) rsb[e] = bload(rsb_r, ok ? 4 * (jj * g.B + b) : kOOB);
+      rb[e] = bload(rx, (int)(base + (unsigned)(e * RSTEP) * cs4));
+      if (SCALED) rsb[e] = bload(rsb_r, (int)(sbase + 4u * (unsigned)(e * RSTEP * g.B)));
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][(tr + e * RSTEP) * LDKW + tk] = SCALED ? ra[e] * rsa[e] : ra[e];
+    for (int e = 0; e < EA; ++e) {
+      const int slot = tid + e * kThreads;
+      if (slot < A4) {
+        f32x4 v = ra[e];
+        if (SCALED) v *= rsa[e];
+        float* d = &As[buf][(slot >> 3) * LDKW + 4 * (slot & 7)];
+        *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
+        *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
+      }
+    }
 #pragma unroll
     for (int e = 0; e < EB; ++e) Bs[buf][(tr + e * RSTEP) * LDKW + tk] = SCALED ? rb[e] * rsb[e] : rb[e];
   };
@@ -528,7 +579,7 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
     bn = 64;
   }
   const int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
-  return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, wgrad_block_target(), 32);
+  return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, wgrad_block_target(), 256);
 }
 
 __global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int N, int ohw, int B,
