@@ -28,7 +28,8 @@ CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
-                ("B", "Cin", "H", "W", "Cout", "OH", "OW", "KH", "KW", "stride", "pad", "pad_mode", "transposed")]
+                ("B", "Cin", "H", "W", "Cout", "OH", "OW", "KH", "KW", "stride", "pad", "pad_mode", "transposed",
+                 "packed_w")]
 
 
 class GTile(ctypes.Structure):
@@ -41,6 +42,8 @@ class GTile(ctypes.Structure):
 _SIGS = {
     "ganamd_version": (ctypes.c_char_p, []),
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
+    "ganamd_conv_pack_bytes": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
+    "ganamd_conv_pack": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, vp]),
     "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),

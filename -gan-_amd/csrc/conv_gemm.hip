@@ -630,15 +630,22 @@ hipError_t dispatch_conv_tile(const ConvArgs& p, const Plan& pl, float* slab, hi
   }
 }
 
-// p.w/sm/sc/st describe the weights as stored; `packed` (pack_bytes) receives the GEMM-order copy.
-hipError_t dispatch_conv(ConvArgs p, float* packed, float* slab, hipStream_t st) {
+void launch_pack(const ConvArgs& p, int mpad, int ckp, float* packed, hipStream_t st) {
+  hipLaunchKernelGGL(pack_a_kernel, dim3(grid1d((long)mpad * p.T * ckp)), dim3(256), 0, st, p.w, p.sm, p.sc, p.st,
+                     p.M, p.Ck, p.T, mpad, ckp, packed);
+}
+
+// p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
+// GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
+hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
   const Plan pl = conv_plan(p.M, p.N, p.Ck, p.T);
-  if ((pl.splits > 1 && !slab) || !packed) return hipErrorInvalidValue;
+  if ((pl.splits > 1 && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
   const int mpad = (p.M + pl.bm - 1) / pl.bm * pl.bm;
   p.Ckp = (p.Ck + BK - 1) / BK * BK;
-  hipLaunchKernelGGL(pack_a_kernel, dim3(grid1d((long)mpad * p.T * p.Ckp)), dim3(256), 0, st, p.w, p.sm, p.sc, p.st,
-                     p.M, p.Ck, p.T, mpad, p.Ckp, packed);
-  p.w = packed;
+  if (!prepacked) {
+    launch_pack(p, mpad, p.Ckp, packed, st);
+    p.w = packed;
+  }
   p.w_bytes = 4 * mpad * p.T * p.Ckp;
   const bool s = p.g.scale != nullptr;
   switch (p.g.mode) {
@@ -715,12 +722,60 @@ static void dgrad_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* 
   *N = d->B * hp * wp;
 }
 
+// The A operand (weights) of the fwd / dgrad GEMM as stored: A(m, t, c) = w[m*sm + c*sc + t*st].
+static void a_operand(const ganamd_conv_desc* d, int op, int* M, int* Ck, int* T, int* sm, int* sc) {
+  *T = d->KH * d->KW;
+  if (op == GANAMD_CONV_FWD) {
+    *M = d->Cout;
+    *Ck = d->Cin;
+    if (d->transposed) {  // weights [Cin][Cout][KH][KW], transposed gather
+      *sm = *T;
+      *sc = d->Cout * *T;
+    } else {              // weights [Cout][Cin][KH][KW]
+      *sm = d->Cin * *T;
+      *sc = *T;
+    }
+  } else {
+    *M = d->Cin;
+    *Ck = d->Cout;
+    if (d->transposed) {  // dX of ConvT: plain conv of gy with W viewed [Cin][Cout][KH][KW]
+      *sm = d->Cout * *T;
+      *sc = *T;
+    } else {              // dX of conv: transposed gather, W[co][ci][t] as A(ci, t, co)
+      *sm = *T;
+      *sc = d->Cin * *T;
+    }
+  }
+}
+
 static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
   if (d->transposed || d->pad == 0) return 0;
   return sizeof(float) * (size_t)d->Cin * d->B * (d->H + 2 * d->pad) * (d->W + 2 * d->pad);
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes) {
+  if (!desc_ok(d) || !bytes || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
+  int M, Ck, T, sm, sc;
+  a_operand(d, op, &M, &Ck, &T, &sm, &sc);
+  *bytes = pack_bytes(M, Ck, T);
+  return GANAMD_OK;
+}
+
+int ganamd_conv_pack(const ganamd_conv_desc* d, int op, const float* w, float* packed, hipStream_t stream) {
+  if (!desc_ok(d) || !w || !packed || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
+  ConvArgs p{};
+  int sm, sc;
+  a_operand(d, op, &p.M, &p.Ck, &p.T, &sm, &sc);
+  p.w = w;
+  p.sm = sm;
+  p.sc = sc;
+  p.st = 1;
+  const Plan pl = conv_plan(p.M, 1, p.Ck, p.T);
+  launch_pack(p, (p.M + pl.bm - 1) / pl.bm * pl.bm, (p.Ck + BK - 1) / BK * BK, packed, stream);
+  return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+}
 
 int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   if (!desc_ok(d) || !bytes) return GANAMD_EINVAL;
@@ -729,11 +784,12 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   if (op == GANAMD_CONV_FWD) {
     fwd_gemm(d, &M, &N, &Ck, &T);
     const Plan pl = conv_plan(M, N, Ck, T);
-    *bytes = align256(pack_bytes(M, Ck, T)) + (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) +
+             (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
     const Plan pl = conv_plan(M, N, Ck, T);
-    *bytes = align256(pack_bytes(M, Ck, T)) + align256(dgrad_pad_bytes(d)) +
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
              (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
@@ -752,20 +808,18 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
                     hipStream_t stream) {
-  if (!desc_ok(d) || !x || !w || !y || !workspace) return GANAMD_EINVAL;
+  if (!desc_ok(d) || !x || !w || !y) return GANAMD_EINVAL;
+  size_t need = 0;
+  ganamd_conv_workspace(d, GANAMD_CONV_FWD, &need);
+  if (need && !workspace) return GANAMD_EINVAL;
   ConvArgs p{};
-  int M, N, Ck, T;
+  int M, N, Ck, T, sm, sc;
   fwd_gemm(d, &M, &N, &Ck, &T);
+  a_operand(d, GANAMD_CONV_FWD, &M, &Ck, &T, &sm, &sc);
   p.w = w;
-  if (d->transposed) {  // weights [Cin][Cout][KH][KW]
-    p.sm = T;
-    p.sc = d->Cout * T;
-  } else {              // weights [Cout][Cin][KH][KW]
-    p.sm = d->Cin * T;
-    p.sc = T;
-  }
+  p.sm = sm;
+  p.sc = sc;
   p.st = 1;
-  p.w_bytes = 4 * d->Cin * d->Cout * T;
   p.M = M;
   p.Ck = Ck;
   p.T = T;
@@ -778,19 +832,25 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
   p.N = N;
   p.ohw = d->OH * d->OW;
   char* ws = static_cast<char*>(workspace);
-  float* slab = reinterpret_cast<float*>(ws + align256(pack_bytes(M, Ck, T)));
-  return dispatch_conv(p, reinterpret_cast<float*>(ws), slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
+  float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))));
+  return dispatch_conv(p, d->packed_w != 0, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale, float alpha,
                       float* gx, void* workspace, hipStream_t stream) {
-  if (!desc_ok(d) || !gy || !w || !gx || !workspace) return GANAMD_EINVAL;
-  int M, N, Ck, T;
+  if (!desc_ok(d) || !gy || !w || !gx) return GANAMD_EINVAL;
+  size_t need = 0;
+  ganamd_conv_workspace(d, GANAMD_CONV_DGRAD, &need);
+  if (need && !workspace) return GANAMD_EINVAL;
+  int M, N, Ck, T, sm, sc;
   dgrad_gemm(d, &M, &N, &Ck, &T);
+  a_operand(d, GANAMD_CONV_DGRAD, &M, &Ck, &T, &sm, &sc);
   ConvArgs p{};
   p.w = w;
+  p.sm = sm;
+  p.sc = sc;
   p.st = 1;
-  p.w_bytes = 4 * d->Cin * d->Cout * T;
   p.M = M;
   p.Ck = Ck;
   p.T = T;
@@ -800,27 +860,24 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   p.N = N;
   const size_t pad_bytes = dgrad_pad_bytes(d);
   char* ws = static_cast<char*>(workspace);
-  float* packed = reinterpret_cast<float*>(ws);
-  ws += align256(pack_bytes(M, Ck, T));
+  float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
+  if (!d->packed_w) ws += align256(pack_bytes(M, Ck, T));
   float* slab = reinterpret_cast<float*>(ws + align256(pad_bytes));
+  const bool pre = d->packed_w != 0;
   if (d->transposed) {
     // dX of ConvT = plain zero-padded conv of gy with W viewed [Cin][Cout][KH][KW]
-    p.sm = d->Cout * T;
-    p.sc = T;
     p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, kZero};
     p.y = gx;
     p.ohw = d->H * d->W;
-    return dispatch_conv(p, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+    return dispatch_conv(p, pre, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   // dX of conv = transposed gather of gy into the padded input frame, then fold the pad
-  p.sm = T;
-  p.sc = d->Cin * T;
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
   float* out = pad_bytes ? reinterpret_cast<float*>(ws) : gx;
   p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
   p.y = out;
   p.ohw = Hp * Wp;
-  if (dispatch_conv(p, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+  if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
   if (pad_bytes) {
     const long planes = (long)d->Cin * d->B;
     hipLaunchKernelGGL(fold_pad_kernel, dim3(grid1d(planes * d->H * d->W)), dim3(256), 0, stream, out, gx, planes,

@@ -43,22 +43,27 @@ class Geo:
     pad_mode: int = _lib.PAD_REPLICATE
     transposed: bool = False
 
-    def desc(self):
-        d = _DESC_CACHE.get(self)
+    def desc(self, packed=False):
+        key = (self, packed)
+        d = _DESC_CACHE.get(key)
         if d is None:
             d = _lib.ConvDesc(self.B, self.Cin, self.H, self.W, self.Cout, self.OH, self.OW, self.K, self.K,
-                              self.stride, self.pad, self.pad_mode, int(self.transposed))
-            _DESC_CACHE[self] = d
+                              self.stride, self.pad, self.pad_mode, int(self.transposed), int(packed))
+            _DESC_CACHE[key] = d
         return d
 
-    def ws_bytes(self, op):
-        key = (self, op)
+    def ws_bytes(self, op, packed=False):
+        key = (self, op, packed)
         v = _WS_CACHE.get(key)
         if v is None:
             n = _lib.c_size_t(0)
-            check(LIB.ganamd_conv_workspace(self.desc(), op, n), "conv_workspace")
+            check(LIB.ganamd_conv_workspace(self.desc(packed), op, n), "conv_workspace")
             v = _WS_CACHE[key] = n.value
         return v
+
+    def pack_key(self, op):
+        """What the packed weight operand depends on (not the batch or the spatial size)."""
+        return (op, self.Cin, self.Cout, self.K, self.transposed)
 
 
 _DESC_CACHE: dict = {}
@@ -100,6 +105,53 @@ class FlopCounter:
             cls.launches += 1
 
 
+# ------------------------------------------------------------------------------------------
+# packed weight operands (ganamd_conv_pack), cached per parameter between optimizer steps
+# ------------------------------------------------------------------------------------------
+
+
+class PackCache:
+    """GEMM-order copies of parameter weights, reused by every conv call on the same weight
+    (forward, input-gradient backward, the gradient penalty's double backward) until the weight
+    changes.  A weight changes through (a) the fused optimizer, which calls ``invalidate()``,
+    or (b) torch in-place ops on the Parameter (``load_state_dict``, ``p.copy_``), which bump its
+    version counter.  Only weights that are Parameters (or views of one) are cached.  Under HIP
+    graph capture the pack launches are captured where the cache misses, so replays repack at
+    the same points."""
+
+    epoch = 0
+    entries: dict = {}
+
+    @classmethod
+    def invalidate(cls):
+        cls.epoch += 1
+
+    @classmethod
+    def clear(cls):
+        cls.entries.clear()
+        cls.epoch += 1
+
+    @classmethod
+    def get(cls, geo: "Geo", op: int, w):
+        root = w if w._base is None else w._base
+        if not isinstance(root, torch.nn.Parameter):
+            return None
+        key = (id(root), w.data_ptr(), geo.pack_key(op))
+        e = cls.entries.get(key)
+        if e is not None and e[0] is root and e[1] == root._version and e[2] == cls.epoch:
+            return e[3]
+        n = _lib.c_size_t(0)
+        check(LIB.ganamd_conv_pack_bytes(geo.desc(), op, n), "conv_pack_bytes")
+        packed = torch.empty(n.value // 4, device=w.device, dtype=torch.float32)
+        check(LIB.ganamd_conv_pack(geo.desc(), op, ptr(w), ptr(packed), stream()), "conv_pack")
+        cls.entries[key] = (root, root._version, cls.epoch, packed)
+        return packed
+
+
+def invalidate_packed():
+    PackCache.invalidate()
+
+
 def _need(t, n, what):
     """Host-side operand check before any launch: a wrong size must raise, never fault."""
     if t is not None and t.numel() != n:
@@ -118,10 +170,12 @@ def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0):
     _need(ys, geo.Cout * geo.B, "conv_fwd y_scale")
     FlopCounter.add(geo, "fwd", xs is not None, ys is not None)
     y = torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device, dtype=torch.float32)
-    nb = geo.ws_bytes(_lib.CONV_FWD)
+    pw = PackCache.get(geo, _lib.CONV_FWD, w)
+    packed = pw is not None
+    nb = geo.ws_bytes(_lib.CONV_FWD, packed)
     ws = workspace(nb, x.device) if nb else None
-    check(LIB.ganamd_conv_fwd(geo.desc(), ptr(x), ptr(w), ptr(bias), ptr(xs), ptr(ys), float(alpha), ptr(y),
-                              ptr(ws), stream()), "conv_fwd")
+    check(LIB.ganamd_conv_fwd(geo.desc(packed), ptr(x), ptr(pw if packed else w), ptr(bias), ptr(xs), ptr(ys),
+                              float(alpha), ptr(y), ptr(ws), stream()), "conv_fwd")
     return y
 
 
@@ -131,10 +185,12 @@ def _conv_dgrad(geo: Geo, gy, w, gys=None, alpha=1.0):
     _need(gys, geo.Cout * geo.B, "conv_dgrad gy_scale")
     FlopCounter.add(geo, "dgrad", gys is not None, False)
     gx = torch.empty((geo.Cin, geo.B, geo.H, geo.W), device=gy.device, dtype=torch.float32)
-    nb = geo.ws_bytes(_lib.CONV_DGRAD)
+    pw = PackCache.get(geo, _lib.CONV_DGRAD, w)
+    packed = pw is not None
+    nb = geo.ws_bytes(_lib.CONV_DGRAD, packed)
     ws = workspace(nb, gy.device) if nb else None
-    check(LIB.ganamd_conv_dgrad(geo.desc(), ptr(gy), ptr(w), ptr(gys), float(alpha), ptr(gx), ptr(ws), stream()),
-          "conv_dgrad")
+    check(LIB.ganamd_conv_dgrad(geo.desc(packed), ptr(gy), ptr(pw if packed else w), ptr(gys), float(alpha), ptr(gx),
+                                ptr(ws), stream()), "conv_dgrad")
     return gx
 
 

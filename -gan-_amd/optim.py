@@ -17,6 +17,7 @@ from __future__ import annotations
 import torch
 
 from ._lib import LIB, check, iptr, ptr, stream
+from .ops import invalidate_packed
 
 
 def _never_gets_grad(owner_cls: str, pname: str) -> bool:
@@ -51,6 +52,7 @@ class FlatParams:
             if off < n_train:
                 p.grad = self.grad[off:off + n].view_as(p)
             off += n
+        invalidate_packed()
         module.__dict__["_flat"] = self      # lets the module find its flat buffers (style bank)
 
     def zero_grad(self):
@@ -77,3 +79,4 @@ class FusedAdamW:
         check(LIB.ganamd_adamw(ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.n_train,
                                iptr(self.step_count), float(self.lr), float(self.betas[0]), float(self.betas[1]),
                                float(self.eps), float(self.weight_decay), stream()), "adamw")
+        invalidate_packed()   # packed conv weights (ops.PackCache) are stale now

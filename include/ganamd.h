@@ -49,10 +49,19 @@ typedef struct ganamd_conv_desc {
   int32_t KH, KW, stride, pad;
   int32_t pad_mode;   /* GANAMD_PAD_ZERO | GANAMD_PAD_REPLICATE (ignored when transposed) */
   int32_t transposed;
+  int32_t packed_w;   /* 1: the w argument of conv_fwd/conv_dgrad is already in GEMM order
+                         (ganamd_conv_pack for the same op and geometry); 0: as stored */
 } ganamd_conv_desc;
 
 /* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD). */
 int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
+
+/* The weight operand of conv_fwd / conv_dgrad in GEMM order (rows padded to the tile grid,
+ * channels to whole K-steps, zero filled).  A caller that reuses a weight across calls (the
+ * same parameter in forward, backward and the gradient penalty's double backward) packs it
+ * once per optimizer step and passes packed_w = 1.  op: GANAMD_CONV_FWD or GANAMD_CONV_DGRAD. */
+int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes);
+int ganamd_conv_pack(const ganamd_conv_desc* d, int op, const float* w, float* packed, hipStream_t stream);
 
 /* y[co][b,oh,ow] = alpha * y_scale[co][b] * sum W * (x * x_scale[ci][b]) + bias[co]
  * Replaces: EqualizedConv2d.forward = F.conv2d(ReplicationPad2d(x), W*c, b)

@@ -347,3 +347,32 @@ def test_grouped_gemm(a_t, b_t, sq):
     got = C.double().cpu()
     ref = torch.cat(want)
     assert rel(got, ref) < 1e-5
+
+
+def test_packed_weight_cache_tracks_updates(ops):
+    """The packed-weight cache (ops.PackCache) never serves a stale weight: after a torch in-place
+    update of the Parameter and after a fused AdamW step the conv sees the new values."""
+    from gan_amd.optim import FusedAdamW
+    torch.manual_seed(0)
+    geo = ops.conv_geo(4, 8, 16, 16, 12, 3, 1, 1)
+    lin = torch.nn.Module()
+    lin.w = torch.nn.Parameter(torch.randn(12, 8, 3, 3, device="cuda"))
+    x = torch.randn(8, 4, 16, 16, device="cuda")
+
+    def run():
+        return ops.conv2d(x, lin.w, None, geo, 0.5)
+
+    def fresh():   # a plain tensor is never cached
+        return ops.conv2d(x, lin.w.detach().clone(), None, geo, 0.5)
+
+    y0 = run()
+    assert rel(run(), y0) == 0
+    with torch.no_grad():
+        lin.w.mul_(2)
+    assert rel(run(), 2 * y0) < 1e-6
+    opt = FusedAdamW(lin, lr=0.1)
+    y1 = run()
+    (y1 * torch.randn_like(y1)).sum().backward()
+    opt.step()
+    assert rel(run(), fresh()) == 0
+    assert rel(run(), y1) > 1e-3
