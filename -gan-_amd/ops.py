@@ -113,8 +113,9 @@ class FlopCounter:
 class PackCache:
     """GEMM-order copies of parameter weights, reused by every conv call on the same weight
     (forward, input-gradient backward, the gradient penalty's double backward) until the weight
-    changes.  A weight changes through (a) the fused optimizer, which calls ``invalidate()``,
-    or (b) torch in-place ops on the Parameter (``load_state_dict``, ``p.copy_``), which bump its
+    changes.  A weight changes through (a) the fused optimizer, which bumps the epoch of its flat
+    buffer (``FlatParams.epoch``; parameters outside one follow the global ``invalidate()``), or
+    (b) torch in-place ops on the Parameter (``load_state_dict``, ``p.copy_``), which bump its
     version counter.  Only weights that are Parameters (or views of one) are cached.  Under HIP
     graph capture the pack launches are captured where the cache misses, so replays repack at
     the same points."""
@@ -137,14 +138,17 @@ class PackCache:
         if not isinstance(root, torch.nn.Parameter):
             return None
         key = (id(root), w.data_ptr(), geo.pack_key(op))
+        # parameters living in an optimizer's flat buffer are stale only after THAT optimizer steps
+        flat = getattr(root, "_gan_flat", None)
+        epoch = (id(flat), flat.epoch) if flat is not None else cls.epoch
         e = cls.entries.get(key)
-        if e is not None and e[0] is root and e[1] == root._version and e[2] == cls.epoch:
+        if e is not None and e[0] is root and e[1] == root._version and e[2] == epoch:
             return e[3]
         n = _lib.c_size_t(0)
         check(LIB.ganamd_conv_pack_bytes(geo.desc(), op, n), "conv_pack_bytes")
         packed = torch.empty(n.value // 4, device=w.device, dtype=torch.float32)
         check(LIB.ganamd_conv_pack(geo.desc(), op, ptr(w), ptr(packed), stream()), "conv_pack")
-        cls.entries[key] = (root, root._version, cls.epoch, packed)
+        cls.entries[key] = (root, root._version, epoch, packed)
         return packed
 
 

@@ -52,6 +52,8 @@ class FlatParams:
             if off < n_train:
                 p.grad = self.grad[off:off + n].view_as(p)
             off += n
+            p._gan_flat = self
+        self.epoch = 0
         invalidate_packed()
         module.__dict__["_flat"] = self      # lets the module find its flat buffers (style bank)
 
@@ -79,4 +81,4 @@ class FusedAdamW:
         check(LIB.ganamd_adamw(ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.n_train,
                                iptr(self.step_count), float(self.lr), float(self.betas[0]), float(self.betas[1]),
                                float(self.eps), float(self.weight_decay), stream()), "adamw")
-        invalidate_packed()   # packed conv weights (ops.PackCache) are stale now
+        f.epoch += 1   # packed conv weights of these parameters (ops.PackCache) are stale now
