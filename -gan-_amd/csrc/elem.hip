@@ -443,27 +443,42 @@ __global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int
 }
 
 // ---------------------------------------------------------------- separable resampling
+// Separable resampling through LDS: a workgroup stages `ppb` whole input planes, applies the
+// column table along rows into an LDS intermediate [IH][OW], then the row table along columns
+// straight to global memory.  HBM traffic = one read of x + one write of y; the tap tables
+// (ELL: KR/KC taps per output row/column, zero-weight padding) stay in L1.
 __global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict__ x, long planes, int IH, int IW,
                                                          float* __restrict__ y, int OH, int OW,
                                                          const int32_t* __restrict__ ri, const float* __restrict__ rw,
                                                          int KR, const int32_t* __restrict__ ci,
-                                                         const float* __restrict__ cw, int KC) {
-  const long total = planes * OH * OW;
-  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < total; i += (long)gridDim.x * kNT) {
-    const int ow = (int)(i % OW);
-    const int oh = (int)((i / OW) % OH);
-    const long p = i / ((long)OH * OW);
-    const float* xp = x + p * IH * IW;
+                                                         const float* __restrict__ cw, int KC, int ppb) {
+  extern __shared__ float lds[];
+  const long p0 = (long)blockIdx.x * ppb;
+  const int np = (int)min((long)ppb, planes - p0);
+  float* xs = lds;
+  float* ts = lds + ppb * IH * IW;
+  const int nin = np * IH * IW;
+  const float* xg = x + p0 * IH * IW;
+  for (int i = threadIdx.x; i < nin; i += kNT) xs[i] = xg[i];
+  __syncthreads();
+  const int nt = np * IH * OW;
+  for (int i = threadIdx.x; i < nt; i += kNT) {
+    const int ow = i % OW, r = i / OW;
+    const float* xr = xs + r * IW;
     float acc = 0.f;
-    for (int a = 0; a < KR; ++a) {
-      const float wr = rw[oh * KR + a];
-      if (wr == 0.f) continue;
-      const float* xr = xp + (long)ri[oh * KR + a] * IW;
-      float racc = 0.f;
-      for (int b = 0; b < KC; ++b) racc += cw[ow * KC + b] * xr[ci[ow * KC + b]];
-      acc += wr * racc;
-    }
-    y[i] = acc;
+    for (int b = 0; b < KC; ++b) acc += cw[ow * KC + b] * xr[ci[ow * KC + b]];
+    ts[i] = acc;
+  }
+  __syncthreads();
+  const int ohw = OH * OW, no = np * ohw;
+  float* yg = y + p0 * ohw;
+  for (int i = threadIdx.x; i < no; i += kNT) {
+    const int ow = i % OW, r = i / OW;
+    const int oh = r % OH, pl = r / OH;
+    const float* tp = ts + pl * IH * OW + ow;
+    float acc = 0.f;
+    for (int a = 0; a < KR; ++a) acc += rw[oh * KR + a] * tp[ri[oh * KR + a] * OW];
+    yg[i] = acc;
   }
 }
 
@@ -575,8 +590,14 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
 int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
                       const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t st) {
   if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;
-  hipLaunchKernelGGL(resample2d_kernel, dim3(grid_for(planes * OH * OW)), dim3(kNT), 0, st, x, planes, IH, IW, y, OH,
-                     OW, ri, rw, KR, ci, cw, KC);
+  // planes per workgroup: >= ~2K staged inputs, LDS <= 48 KB (3 workgroups per CU)
+  const long per_plane = (long)IH * IW + (long)IH * OW;
+  if (per_plane * 4 > 48 * 1024) return GANAMD_EINVAL;
+  int ppb = (int)std::max<long>(1, 2048 / ((long)IH * IW));
+  ppb = (int)std::min<long>(ppb, (48 * 1024) / (4 * per_plane));
+  const long blocks = (planes + ppb - 1) / ppb;
+  hipLaunchKernelGGL(resample2d_kernel, dim3((unsigned)blocks), dim3(kNT), (size_t)(4 * ppb * per_plane), st, x,
+                     planes, IH, IW, y, OH, OW, ri, rw, KR, ci, cw, KC, ppb);
   return ok(hipGetLastError());
 }
 

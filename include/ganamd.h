@@ -129,7 +129,8 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
  * discriminator_9_4.py:56-72), bicubic x2 / x1/2 with A=-0.75 and clamped taps
  * (generator_13_5.py:160, discriminator_9_4.py:81), AdaptiveAvgPool2d(5)
  * (generator_13_5.py:44,355; discriminator_9_4.py:86), their compositions and, with the
- * transposed tables, their adjoints (backward).
+ * transposed tables, their adjoints (backward).  One plane plus its row-pass intermediate
+ * (IH*IW + IH*OW floats) must fit 48 KB of LDS, else GANAMD_EINVAL.
  * ------------------------------------------------------------------------------------- */
 int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
                       const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t stream);
