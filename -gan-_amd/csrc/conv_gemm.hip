@@ -41,7 +41,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int BK = 16;        // conv K-step (taps x channels)
+#ifndef GANAMD_BK
+#define GANAMD_BK 16
+#endif
+constexpr int BK = GANAMD_BK; // conv K-step (taps x channels)
 constexpr int LDK = BK + 2;   // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
 constexpr int BKW = 32;       // wgrad K-step (pixels): a half-wave reads one full 128-byte line
 constexpr int LDKW = BKW + 2;
@@ -223,14 +226,15 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
   const int kt1 = min(kt_total, kt0 + p.kt_per_split);
   if (kt0 >= kt1) return;
 
-  // A slots: row m = slot/4, k = 4*(slot%4) (+ kt*BK): contiguous along the packed row
+  // A slots: row m = slot/SPR, k = 4*(slot%SPR) (+ kt*BK): contiguous along the packed row
+  constexpr int SPR = BK / 4;
   const int Krow = p.T * p.Ckp;
   const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
   int a_off[EA];
 #pragma unroll
   for (int e = 0; e < EA; ++e) {
     const int slot = tid + e * kThreads;
-    a_off[e] = 4 * ((m0 + (slot >> 2)) * Krow + 4 * (slot & 3));
+    a_off[e] = 4 * ((m0 + slot / SPR) * Krow + 4 * (slot % SPR));
   }
 
   // B: pixel n = n0 + tid % BN, channels c0 + kg*KPT .. +KPT-1 of the K-step
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     for (int e = 0; e < EA; ++e) {
       const int slot = tid + e * kThreads;
       if (slot < A4) {
-        float* d = &As[buf][(slot >> 2) * LDK + 4 * (slot & 3)];
+        float* d = &As[buf][(slot / SPR) * LDK + 4 * (slot % SPR)];
         *reinterpret_cast<f32x2*>(d) = f32x2{ra[e][0], ra[e][1]};
         *reinterpret_cast<f32x2*>(d + 2) = f32x2{ra[e][2], ra[e][3]};
       }
@@ -305,7 +309,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn);
+#pragma unroll
+    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
