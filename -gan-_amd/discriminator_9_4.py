@@ -69,16 +69,21 @@ class MiniBatchStdDev(nn.Module):
     """discriminator_9_4.py:42-54.  The reference groups NCHW ``x.view(4, -1)``: element
     (b, c, h, w) belongs to group b // (B/4); in CNHW that is ``x.view(C, 4, B/4, H, W)``."""
 
+    segments = 1     # set by Discriminator.forward: the batch is this many independent mini-batches
+
     def __init__(self, group_size: int = 4):
         super().__init__()
         self.group_size = group_size
 
     def forward(self, x):
         C, B, H, W = x.shape
-        assert B % self.group_size == 0
-        g = x.reshape(C, self.group_size, B // self.group_size, H, W)
-        std = torch.sqrt(g.var(dim=1) + 1e-8).mean()
-        return torch.cat([x, std.view(1, 1, 1, 1).expand(1, B, H, W)], dim=0)
+        S = self.segments
+        assert B % S == 0 and (B // S) % self.group_size == 0
+        Bs = B // S
+        g = x.reshape(C, S, self.group_size, Bs // self.group_size, H, W)
+        std = torch.sqrt(g.var(dim=2) + 1e-8).mean(dim=(0, 2, 3, 4))          # one value per segment
+        feat = std.view(1, S, 1, 1, 1).expand(1, S, Bs, H, W).reshape(1, B, H, W)
+        return torch.cat([x, feat], dim=0)
 
 
 class Smooth(nn.Module):
@@ -194,8 +199,15 @@ class Discriminator(nn.Module):
         n = 2 * 2 * (16 * f + 1)
         self.fc = nn.Sequential(EqualizedLinear(n, n), nn.PReLU(n), EqualizedLinear(n, 1))
 
-    def forward(self, input):
+    def forward(self, input, segments: int = 1):
+        """``segments`` > 1: ``input`` is that many independent mini-batches stacked along the
+        batch (the critic step runs its real and fake batches as one pass); every layer is
+        per-sample except MiniBatchStdDev, which is computed per segment, so the output equals
+        the per-segment calls concatenated."""
         B = input.shape[0]
+        for mod in self.conv:
+            if isinstance(mod, MiniBatchStdDev):
+                mod.segments = segments
         x = ops.nchw_to_cnhw(input)
         for mod in self.conv:
             x = prelu(x, mod.weight) if isinstance(mod, nn.PReLU) else mod(x)

@@ -105,13 +105,16 @@ class Train:
         with torch.no_grad():
             gen_imgs = self._generate(z)
         gen_imgs.requires_grad_()
-        pred_r = self.discriminator(images)
+        # The real and fake batches go through the critic as ONE pass of 2B samples (two
+        # MiniBatchStdDev segments, see Discriminator.forward): the critic is per-sample apart
+        # from that layer, so the outputs and the summed weight gradients are those of the
+        # reference's two forward/backward calls (wgangp.py:60-66), with one backward.  The input
+        # gradient the reference leaves in gen_imgs.grad is never read (dead work, skipped).
+        pred = self.discriminator(torch.cat([images, gen_imgs.detach()]), segments=2)
+        pred_r, pred_f = pred[:b_size], pred[b_size:]
         real_loss = -torch.mean(pred_r)
-        real_loss.backward()
-        # the input gradient this backward would leave in gen_imgs.grad is never read (dead work)
-        pred_f = self.discriminator(gen_imgs.detach())
         fake_loss = torch.mean(pred_f)
-        fake_loss.backward()
+        (real_loss + fake_loss).backward()
         gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
         gp.backward()
         return real_loss, fake_loss, gp

@@ -208,6 +208,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     secs = float(t)
 
+    if rank == 0 and args.mode == "graph" and world == 1:
+        # breakdown (outside the timed region): one critic-step graph, one generator-step graph
+        parts = {}
+        for name, g in (("critic_step", gd), ("generator_step", gg)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            parts[name] = round(e0.elapsed_time(e1), 1)
+        print(f"[bench] ms per graph: {parts}", file=sys.stderr, flush=True)
     if rank == 0:
         print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
               f"issued GEMM launches/iter {ops.FlopCounter.launches}", file=sys.stderr, flush=True)

@@ -170,3 +170,16 @@ def test_style_bank_matches_modules(gan, P):
     assert rel_err(b1.numpy(), b0.numpy()) < 1e-5
     med, p99, mx, vec = grad_norm_stats(r1, r0)
     assert med < 2e-3 and vec < 2e-3, (med, p99, mx, vec)
+
+
+def test_d_segments_equal_separate_calls(gan, P):
+    """D(cat(a, b), segments=2) == cat(D(a), D(b)): the critic step's batched real+fake pass."""
+    D = make_D(gan, P)
+    g = torch.Generator().manual_seed(9)
+    a = torch.randn(8, 3, 64, 64, generator=g).to(DEV)
+    b = torch.randn(8, 3, 64, 64, generator=g).to(DEV)
+    with torch.no_grad():
+        sep = torch.cat([D(a), D(b)])
+        both = D(torch.cat([a, b]), segments=2)
+        assert rel_err(both.cpu().numpy(), sep.cpu().numpy()) < 1e-5
+        assert rel_err(D(a).cpu().numpy(), sep[:8].cpu().numpy()) == 0   # segments reset to 1
