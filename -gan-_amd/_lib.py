@@ -44,6 +44,11 @@ _SIGS = {
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_pack_bytes": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_pack": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, vp]),
+    "ganamd_conv_fwd_ex": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp, vp, vp, vp]),
+    "ganamd_mix_fwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp]),
+    "ganamd_mix_bwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp, vp, vp, vp, vp, vp]),
+    "ganamd_add_prelu": (c_int, [vp, vp, vp, c_int, c_long, vp, vp]),
+    "ganamd_scale_add": (c_int, [vp, vp, vp, c_long, c_long, vp, vp]),
     "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),

@@ -120,6 +120,9 @@ struct ConvArgs {
   float* y;            // Y[m][n]
   const float* bias;   // [M] or null
   const float* oscale; // [M][B] or null
+  const float* noise;  // [M][N] or null: + noise_scale[m] * noise[m][n]   (StyleConv noise)
+  const float* noise_scale;
+  const float* act;    // [M] or null: PReLU with these slopes, applied last
   float alpha;
   int N, ohw;          // N = B*OH*OW
   int kt_per_split;
@@ -334,6 +337,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
         if (finish) {
           if (p.oscale) v *= p.oscale[m * g.B + b];
           if (p.bias) v += p.bias[m];
+          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.N + n];
+          if (p.act) v = v > 0.f ? v : p.act[m] * v;
         }
         out[(long)m * p.N + n] = v;
       }
@@ -521,6 +526,45 @@ __global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict_
   }
 }
 
+// Input gradient of a small-map stride-1 conv from the per-tap products Z[(ci,t)][b,oh,ow]
+// (the "scatter" form of dgrad, see ganamd_conv_dgrad): every input pixel sums, per tap, the
+// outputs whose (padded) receptive field reads it -- one output per tap in the interior, a
+// run of outputs at a replication-padded edge.
+__global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict__ gx, int C, int B, int H, int W,
+                                  int OH, int OW, int KH, int KW, int pad, int replicate) {
+  const long total = (long)C * B * H * W;
+  const int T = KH * KW;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % W);
+    const int i = (int)((idx / W) % H);
+    const int b = (int)((idx / ((long)W * H)) % B);
+    const int c = (int)(idx / ((long)W * H * B));
+    float acc = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      int h0 = i - kh + pad, h1 = h0;                       // outputs oh with pad-map(oh + kh - pad) == i
+      if (replicate) {
+        if (i == 0) h0 = 0;
+        if (i == H - 1) h1 = OH - 1;
+      }
+      h0 = max(h0, 0);
+      h1 = min(h1, OH - 1);
+      for (int kw = 0; kw < KW; ++kw) {
+        int w0 = j - kw + pad, w1 = w0;
+        if (replicate) {
+          if (j == 0) w0 = 0;
+          if (j == W - 1) w1 = OW - 1;
+        }
+        w0 = max(w0, 0);
+        w1 = min(w1, OW - 1);
+        const float* z = Z + ((long)(c * T + kh * KW + kw) * B + b) * OH * OW;
+        for (int oh = h0; oh <= h1; ++oh)
+          for (int ow = w0; ow <= w1; ++ow) acc += z[oh * OW + ow];
+      }
+    }
+    gx[idx] = acc;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------------
@@ -548,7 +592,11 @@ struct Plan {
 };
 
 int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
-int conv_bn(int bm) { return bm == 32 ? 256 : 128; }
+int conv_wide_min_n() {
+  static const int v = env_int("GANAMD_CONV_WIDE", 0);   // N at/above which 256-wide tiles are used (0: never)
+  return v;
+}
+int conv_bn(int bm, int N) { return (bm == 32 || (conv_wide_min_n() > 0 && N >= conv_wide_min_n())) ? 256 : 128; }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
 
 Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_splits) {
@@ -565,7 +613,7 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_spl
 }
 
 Plan conv_plan(int M, int N, int Ck, int T) {
-  const int bm = conv_bm(M), bn = conv_bn(bm);
+  const int bm = conv_bm(M), bn = conv_bn(bm, N);
   const int tiles = ((N + bn - 1) / bn) * ((M + bm - 1) / bm);
   return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, conv_block_target(), 16);
 }
@@ -589,7 +637,8 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
 
 __global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int N, int ohw, int B,
                                          const float* __restrict__ oscale, const float* __restrict__ bias,
-                                         float* __restrict__ y) {
+                                         const float* __restrict__ noise, const float* __restrict__ noise_scale,
+                                         const float* __restrict__ act, float* __restrict__ y) {
   const long total = (long)M * N;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     float v = 0.f;
@@ -597,6 +646,8 @@ __global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, 
     const int m = (int)(i / N);
     if (oscale) v *= oscale[m * B + (int)(i % N) / ohw];
     if (bias) v += bias[m];
+    if (noise) v += noise_scale[m] * noise[i];
+    if (act) v = v > 0.f ? v : act[m] * v;
     y[i] = v;
   }
 }
@@ -621,14 +672,21 @@ hipError_t launch_conv(ConvArgs p, const Plan& pl, float* slab, hipStream_t st) 
                      st, p);
   if (pl.splits > 1)
     hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.N)), dim3(256), 0, st, slab, pl.splits,
-                       p.M, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.y);
+                       p.M, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act, p.y);
   return hipGetLastError();
 }
 
 template <int MODE, bool BSCALE>
 hipError_t dispatch_conv_tile(const ConvArgs& p, const Plan& pl, float* slab, hipStream_t st) {
+  if (pl.bn == 256) {
+    switch (pl.bm) {
+      case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
+      case 64: return launch_conv<64, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
+      case 96: return launch_conv<96, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
+      default: return launch_conv<128, 256, 2, 2, MODE, BSCALE>(p, pl, slab, st);
+    }
+  }
   switch (pl.bm) {
-    case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
     case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE>(p, pl, slab, st);
     default: return launch_conv<128, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
@@ -719,12 +777,30 @@ static void fwd_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T)
   *T = d->KH * d->KW;
 }
 
+// Small maps (<= 10x10), stride 1: dgrad as a plain GEMM over the conv's OUTPUT pixels,
+// Z[(ci,t)][n] = sum_co W[co][ci][t] * gy[co][n], then dgrad_fold_kernel.  The transposed
+// gather into the padded frame would feed the MFMAs mostly zero taps there (a 4x4 map's 6x6
+// frame: 2.25x the work; a valid 3x3 conv on 5x5: 2.8x).
+static bool dgrad_scatter(const ganamd_conv_desc* d) {
+  return !d->transposed && d->stride == 1 && d->KH * d->KW > 1 && d->H * d->W <= 100;
+}
+
 static void dgrad_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T) {
-  *M = d->Cin;
   *Ck = d->Cout;
+  if (dgrad_scatter(d)) {
+    *M = d->Cin * d->KH * d->KW;
+    *T = 1;
+    *N = d->B * d->OH * d->OW;
+    return;
+  }
+  *M = d->Cin;
   *T = d->KH * d->KW;
   const int hp = d->transposed ? d->H : d->H + 2 * d->pad, wp = d->transposed ? d->W : d->W + 2 * d->pad;
   *N = d->B * hp * wp;
+}
+
+static size_t dgrad_scatter_bytes(const ganamd_conv_desc* d) {
+  return dgrad_scatter(d) ? sizeof(float) * (size_t)d->Cin * d->KH * d->KW * d->B * d->OH * d->OW : 0;
 }
 
 // The A operand (weights) of the fwd / dgrad GEMM as stored: A(m, t, c) = w[m*sm + c*sc + t*st].
@@ -740,6 +816,12 @@ static void a_operand(const ganamd_conv_desc* d, int op, int* M, int* Ck, int* T
       *sm = d->Cin * *T;
       *sc = *T;
     }
+  } else if (dgrad_scatter(d)) {  // Z GEMM: A((ci,t), co) = W[co][ci][t]
+    *M = d->Cin * *T;
+    *Ck = d->Cout;
+    *sm = 1;
+    *sc = d->Cin * *T;
+    *T = 1;
   } else {
     *M = d->Cin;
     *Ck = d->Cout;
@@ -754,7 +836,7 @@ static void a_operand(const ganamd_conv_desc* d, int op, int* M, int* Ck, int* T
 }
 
 static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
-  if (d->transposed || d->pad == 0) return 0;
+  if (d->transposed || d->pad == 0 || dgrad_scatter(d)) return 0;
   return sizeof(float) * (size_t)d->Cin * d->B * (d->H + 2 * d->pad) * (d->W + 2 * d->pad);
 }
 
@@ -795,7 +877,7 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
     const Plan pl = conv_plan(M, N, Ck, T);
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
-             (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
+             align256(dgrad_scatter_bytes(d)) + (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
     T = d->KH * d->KW;
@@ -813,7 +895,14 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
                     hipStream_t stream) {
-  if (!desc_ok(d) || !x || !w || !y) return GANAMD_EINVAL;
+  return ganamd_conv_fwd_ex(d, x, w, bias, x_scale, y_scale, alpha, nullptr, nullptr, nullptr, y, workspace, stream);
+}
+
+int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
+                       const float* x_scale, const float* y_scale, float alpha, const float* noise,
+                       const float* noise_scale, const float* act_alpha, float* y, void* workspace,
+                       hipStream_t stream) {
+  if (!desc_ok(d) || !x || !w || !y || (noise && !noise_scale)) return GANAMD_EINVAL;
   size_t need = 0;
   ganamd_conv_workspace(d, GANAMD_CONV_FWD, &need);
   if (need && !workspace) return GANAMD_EINVAL;
@@ -833,6 +922,9 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
   p.y = y;
   p.bias = bias;
   p.oscale = y_scale;
+  p.noise = noise;
+  p.noise_scale = noise_scale;
+  p.act = act_alpha;
   p.alpha = alpha;
   p.N = N;
   p.ohw = d->OH * d->OW;
@@ -867,8 +959,19 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
   if (!d->packed_w) ws += align256(pack_bytes(M, Ck, T));
-  float* slab = reinterpret_cast<float*>(ws + align256(pad_bytes));
+  float* slab = reinterpret_cast<float*>(ws + align256(pad_bytes) + align256(dgrad_scatter_bytes(d)));
   const bool pre = d->packed_w != 0;
+  if (dgrad_scatter(d)) {
+    float* Z = reinterpret_cast<float*>(ws);
+    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->OH, d->OW, 1, 1, 0, kZero};
+    p.y = Z;
+    p.ohw = d->OH * d->OW;
+    if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+    const long total = (long)d->Cin * d->B * d->H * d->W;
+    hipLaunchKernelGGL(dgrad_fold_kernel, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H, d->W,
+                       d->OH, d->OW, d->KH, d->KW, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
+    return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  }
   if (d->transposed) {
     // dX of ConvT = plain zero-padded conv of gy with W viewed [Cin][Cout][KH][KW]
     p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, d->stride, d->pad, kZero};

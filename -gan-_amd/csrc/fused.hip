@@ -1,0 +1,197 @@
+// Fused per-plane elementwise kernels of the generator / critic blocks (gfx950).
+//
+// Tensors are CNHW, i.e. `planes` = C*B contiguous planes of HW floats; a per-(channel, sample)
+// coefficient vector [C][B] is indexed by the plane number.  These kernels replace chains of
+// 3-6 torch elementwise launches (and their full-tensor round trips through HBM):
+//   mix        y = sum_m att[m] * f_m                 SK mixing (generator_13_5.py:80-89,165-170,196-202)
+//   mix_bwd    gf_m = g * att[m],  gatt[m] = <g, f_m>_plane   (one pass over g and the f_m)
+//   add_prelu  y = PReLU(a + b)                       ResnetInit outputs (generator_13_5.py:343-349)
+//   scale_add  y = r + x * s                          SE gating + residual (generator_13_5.py:455-466,
+//                                                     discriminator_9_4.py:158-161); r may be null
+// All HBM-bound: one read of each input and one write of each output.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/ganamd.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kNT = 256;
+
+inline int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + kNT - 1) / kNT, 16384)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+struct Ptr4 {
+  const float* p[4];
+};
+struct MPtr4 {
+  float* p[4];
+};
+
+// y = sum_m att[m][plane] * f_m ; 4 elements per thread when HW % 4 == 0
+template <int M, bool VEC>
+__global__ __launch_bounds__(kNT) void mix_fwd_kernel(Ptr4 f, const float* __restrict__ att, long planes, long HW,
+                                                      float* __restrict__ y) {
+  const long n = planes * HW / (VEC ? 4 : 1);
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < n; i += (long)gridDim.x * kNT) {
+    const long p = (VEC ? 4 * i : i) / HW;
+    if (VEC) {
+      f32x4 acc = reinterpret_cast<const f32x4*>(f.p[0])[i] * att[p];
+#pragma unroll
+      for (int m = 1; m < M; ++m) acc += reinterpret_cast<const f32x4*>(f.p[m])[i] * att[m * planes + p];
+      reinterpret_cast<f32x4*>(y)[i] = acc;
+    } else {
+      float acc = f.p[0][i] * att[p];
+#pragma unroll
+      for (int m = 1; m < M; ++m) acc += f.p[m][i] * att[m * planes + p];
+      y[i] = acc;
+    }
+  }
+}
+
+// one wave per plane: gf_m = g * att[m], gatt[m] = sum g * f_m
+template <int M>
+__global__ __launch_bounds__(kNT) void mix_bwd_kernel(Ptr4 f, const float* __restrict__ att, long planes, long HW,
+                                                      const float* __restrict__ g, MPtr4 gf, float* __restrict__ gatt) {
+  const long wave = (blockIdx.x * (long)kNT + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * kNT) >> 6;
+  const int lane = threadIdx.x & 63;
+  for (long p = wave; p < planes; p += nwaves) {
+    const long base = p * HW;
+    float a[M], dot[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      a[m] = att[m * planes + p];
+      dot[m] = 0.f;
+    }
+    for (long i = lane; i < HW; i += 64) {
+      const float gv = g[base + i];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (gf.p[m]) gf.p[m][base + i] = gv * a[m];
+        dot[m] += gv * f.p[m][base + i];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float d = wave_sum(dot[m]);
+      if (lane == 0 && gatt) gatt[m * planes + p] = d;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kNT) void add_prelu_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                        const float* __restrict__ alpha, int C, long L,
+                                                        float* __restrict__ y) {
+  const long n = (long)C * L;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < n; i += (long)gridDim.x * kNT) {
+    const float z = a[i] + b[i];
+    y[i] = z > 0.f ? z : alpha[i / L] * z;
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void scale_add_kernel(const float* __restrict__ x, const float* __restrict__ s,
+                                                        const float* __restrict__ r, long planes, long HW,
+                                                        float* __restrict__ y) {
+  const long n = planes * HW / (VEC ? 4 : 1);
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < n; i += (long)gridDim.x * kNT) {
+    const float sv = s[(VEC ? 4 * i : i) / HW];
+    if (VEC) {
+      f32x4 v = reinterpret_cast<const f32x4*>(x)[i] * sv;
+      if (r) v += reinterpret_cast<const f32x4*>(r)[i];
+      reinterpret_cast<f32x4*>(y)[i] = v;
+    } else {
+      float v = x[i] * sv;
+      if (r) v += r[i];
+      y[i] = v;
+    }
+  }
+}
+
+inline int ok(hipError_t e) { return e == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH; }
+
+bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int M>
+void launch_mix_fwd(const Ptr4& f, const float* att, long planes, long HW, float* y, hipStream_t st) {
+  bool vec = (HW % 4) == 0 && aligned16(y);
+  for (int m = 0; m < M; ++m) vec = vec && aligned16(f.p[m]);
+  const long n = planes * HW / (vec ? 4 : 1);
+  if (vec)
+    hipLaunchKernelGGL((mix_fwd_kernel<M, true>), dim3(grid_for(n)), dim3(kNT), 0, st, f, att, planes, HW, y);
+  else
+    hipLaunchKernelGGL((mix_fwd_kernel<M, false>), dim3(grid_for(n)), dim3(kNT), 0, st, f, att, planes, HW, y);
+}
+
+template <int M>
+void launch_mix_bwd(const Ptr4& f, const float* att, long planes, long HW, const float* g, const MPtr4& gf,
+                    float* gatt, hipStream_t st) {
+  const int blocks = (int)std::min<long>((planes + 3) / 4, 16384);
+  hipLaunchKernelGGL((mix_bwd_kernel<M>), dim3(blocks), dim3(kNT), 0, st, f, att, planes, HW, g, gf, gatt);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ganamd_mix_fwd(int M, const float* f0, const float* f1, const float* f2, const float* f3, const float* att,
+                   long planes, long HW, float* y, hipStream_t st) {
+  const Ptr4 f{{f0, f1, f2, f3}};
+  if (M < 1 || M > 4 || !att || !y || planes <= 0 || HW <= 0) return GANAMD_EINVAL;
+  for (int m = 0; m < M; ++m)
+    if (!f.p[m]) return GANAMD_EINVAL;
+  switch (M) {
+    case 1: launch_mix_fwd<1>(f, att, planes, HW, y, st); break;
+    case 2: launch_mix_fwd<2>(f, att, planes, HW, y, st); break;
+    case 3: launch_mix_fwd<3>(f, att, planes, HW, y, st); break;
+    default: launch_mix_fwd<4>(f, att, planes, HW, y, st); break;
+  }
+  return ok(hipGetLastError());
+}
+
+int ganamd_mix_bwd(int M, const float* f0, const float* f1, const float* f2, const float* f3, const float* att,
+                   long planes, long HW, const float* gy, float* gf0, float* gf1, float* gf2, float* gf3, float* gatt,
+                   hipStream_t st) {
+  const Ptr4 f{{f0, f1, f2, f3}};
+  const MPtr4 gf{{gf0, gf1, gf2, gf3}};
+  if (M < 1 || M > 4 || !att || !gy || planes <= 0 || HW <= 0) return GANAMD_EINVAL;
+  for (int m = 0; m < M; ++m)
+    if (!f.p[m]) return GANAMD_EINVAL;
+  switch (M) {
+    case 1: launch_mix_bwd<1>(f, att, planes, HW, gy, gf, gatt, st); break;
+    case 2: launch_mix_bwd<2>(f, att, planes, HW, gy, gf, gatt, st); break;
+    case 3: launch_mix_bwd<3>(f, att, planes, HW, gy, gf, gatt, st); break;
+    default: launch_mix_bwd<4>(f, att, planes, HW, gy, gf, gatt, st); break;
+  }
+  return ok(hipGetLastError());
+}
+
+int ganamd_add_prelu(const float* a, const float* b, const float* alpha, int C, long L, float* y, hipStream_t st) {
+  if (!a || !b || !alpha || !y || C <= 0 || L <= 0) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(add_prelu_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, a, b, alpha, C, L, y);
+  return ok(hipGetLastError());
+}
+
+int ganamd_scale_add(const float* x, const float* s, const float* r, long planes, long HW, float* y, hipStream_t st) {
+  if (!x || !s || !y || planes <= 0 || HW <= 0) return GANAMD_EINVAL;
+  const bool vec = (HW % 4) == 0 && aligned16(x) && aligned16(r) && aligned16(y);
+  const long n = planes * HW / (vec ? 4 : 1);
+  if (vec)
+    hipLaunchKernelGGL((scale_add_kernel<true>), dim3(grid_for(n)), dim3(kNT), 0, st, x, s, r, planes, HW, y);
+  else
+    hipLaunchKernelGGL((scale_add_kernel<false>), dim3(grid_for(n)), dim3(kNT), 0, st, x, s, r, planes, HW, y);
+  return ok(hipGetLastError());
+}
+
+}  // extern "C"

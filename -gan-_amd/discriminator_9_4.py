@@ -173,7 +173,7 @@ class DiscriminatorBlock(nn.Module):
         if self.downsample:
             d = self.down_sample
             y = prelu(d[1](d[0](y)), d[2].weight)
-        return y * self.se(y)[:, :, None, None] + res
+        return ops.scale_add(y, self.se(y), res)
 
 
 class Discriminator(nn.Module):

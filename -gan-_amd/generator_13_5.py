@@ -77,10 +77,8 @@ def _lin_bn_act(lin, bn, act, x):
 
 
 def _mix(feas, att):
-    y = feas[0] * att[0][:, :, None, None]
-    for f, a in zip(feas[1:], att[1:]):
-        y = y + f * a[:, :, None, None]
-    return y
+    """sum_m att[m] * feas[m] (att: [M, C, B]) -- one fused kernel (ops.mix)."""
+    return ops.mix(feas, att)
 
 
 def _heads(attn, z):
@@ -89,7 +87,7 @@ def _heads(attn, z):
         sub = getattr(attn, f"fc_sub_{i}")
         v = _lin_bn_act(sub[0], sub[1], sub[2], z)
         vecs.append(sub[3](v))
-    return list(torch.softmax(torch.stack(vecs, 0), dim=0).unbind(0))
+    return torch.softmax(torch.stack(vecs, 0), dim=0)          # [M, C, B]
 
 
 class SKAttention_conv(nn.Module):
@@ -229,14 +227,22 @@ class Conv2dWeightModulate(nn.Module):
 
     _bank_sd = None      # (s, d) handed over by the Generator's style bank for this forward
 
-    def forward(self, x, w):
+    def forward(self, x, w, noise=None, noise_scale=None, act=None):
+        """``noise``/``noise_scale``/``act``: the owning StyleConv's noise and the PReLU that follows
+        it (slopes); without autograd they run in the GEMM epilogue, with autograd as separate ops."""
         C, B, H, W = x.shape
         geo = ops.conv_geo(B, C, H, W, self.out_planes, self.k, 1, (self.k - 1) // 2)
         if self._bank_sd is not None:
             s, d = self._bank_sd
-            return ops.ModConv.apply(x, s, d, self.weight.weights, geo, self.weight.scale)
-        s = bn_act(self.to_style[1](self.to_style[0](w)), self.to_style[2], None)   # [Cin, B]
-        return ops.modconv(x, s, self.weight.weights, geo, self.weight.scale)
+        else:
+            s = bn_act(self.to_style[1](self.to_style[0](w)), self.to_style[2], None)   # [Cin, B]
+            d = ops.demod(s, self.weight.weights, self.weight.scale)
+        if not torch.is_grad_enabled():
+            return ops.modconv_fused(x, s, d, self.weight.weights, geo, self.weight.scale, noise, noise_scale, act)
+        y = ops.ModConv.apply(x, s, d, self.weight.weights, geo, self.weight.scale)
+        if noise is not None:
+            y = y + noise_scale[:, None, None, None] * noise
+        return y if act is None else prelu(y, act)
 
 
 class StyleConv(nn.Module):
@@ -252,13 +258,13 @@ class StyleConv(nn.Module):
         self.bias = _normal(out_planes)
         self._hub = None
 
-    def forward(self, x, w):
-        y = self.conv(x, w)
+    def forward(self, x, w, act=None):
+        """``act``: slopes of the PReLU applied to this conv's output by the caller (fused)."""
+        noise = None
         if self.use_noise:
-            C, B, H, W = y.shape
-            noise = self._hub.noise((B, C, H, W))          # CNHW draw of an NCHW-shaped randn
-            y = y + self.scale_noise[:, None, None, None] * noise
-        return y
+            C, B = self.conv.out_planes, x.shape[1]
+            noise = self._hub.noise((B, C, x.shape[2], x.shape[3]))   # CNHW draw of an NCHW-shaped randn
+        return self.conv(x, w, noise, self.scale_noise if self.use_noise else None, act)
 
 
 class SKStyleConv(nn.Module):
@@ -275,7 +281,7 @@ class SKStyleConv(nn.Module):
         self.sk_attention = (SKAttention_conv if image_size > 4 else SKAttention_fc)(out_planes, m)
 
     def forward(self, x, w):
-        feas = [prelu(getattr(self, f"conv_{i}")(x, w), getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
+        feas = [getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
         return _mix(feas, self.sk_attention(feas))
 
 
@@ -297,9 +303,9 @@ class StyleBlock(nn.Module):
         self.conv3 = StyleConv(d_latent, in_planes, out_planes + dense_depth, kernel_size=3)
 
     def forward(self, x, w):
-        x = prelu(self.conv1(x, w), self.activation1.weight)
+        x = self.conv1(x, w, self.activation1.weight)
         if self.m == 1:
-            x = prelu(self.conv2(x, w), self.activation2.weight)
+            x = self.conv2(x, w, self.activation2.weight)
         else:
             x = self.skconv(x, w)
         return self.conv3(x, w)
@@ -325,8 +331,8 @@ class ResnetInit(nn.Module):
         r_t = self.residual_across(x_res, w)
         t_t = self.transient(x_tr, w)
         t_r = self.transient_across(x_tr, w)
-        return (prelu(r_r + t_r, self.activation_residual.weight),
-                prelu(r_t + t_t, self.activation_transient.weight))
+        return (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
+                ops.add_prelu(r_t, t_t, self.activation_transient.weight))
 
 
 class SEBlock_conv(nn.Module):
@@ -406,7 +412,7 @@ class BasicBlock(nn.Module):
         x_tr = x[d:]
         r3, t3 = self.rir_3((x_res, x_tr), w)
         head = r3[:d]
-        feas_res = x[:d] + head * self.se_attention_residual(head)[:, :, None, None]
+        feas_res = ops.scale_add(head, self.se_attention_residual(head), x[:d])
         if self.root:
             sc = prelu(self.shortcut(x, w), self.activation_shortcut.weight)
             return torch.cat([feas_res, t3, sc, r3[d:]], 0)

@@ -63,7 +63,7 @@ class Geo:
 
     def pack_key(self, op):
         """What the packed weight operand depends on (not the batch or the spatial size)."""
-        return (op, self.Cin, self.Cout, self.K, self.transposed)
+        return (op, self.Cin, self.Cout, self.K, self.transposed, self.H, self.W, self.stride, self.pad)
 
 
 _DESC_CACHE: dict = {}
@@ -158,7 +158,7 @@ def invalidate_packed():
 
 def _need(t, n, what):
     """Host-side operand check before any launch: a wrong size must raise, never fault."""
-    if t is not None and t.numel() != n:
+    if t is not None and n is not None and t.numel() != n:
         raise _lib.GanAmdError(f"{what}: expected {n} elements, got {tuple(t.shape)}")
 
 
@@ -513,6 +513,173 @@ def demod(s, w, c, eps=1e-8):
 
 def modconv(x, s, w, geo, c):
     return ModConv.apply(x, s, demod(s, w, c), w, geo, c)
+
+
+# ------------------------------------------------------------------------------------------
+# fused per-plane elementwise ops (csrc/fused.hip)
+# ------------------------------------------------------------------------------------------
+
+
+def _planes(x):
+    C, B = x.shape[0], x.shape[1]
+    return C * B, x.numel() // (C * B)
+
+
+def _scale_rows(x, s, r=None):
+    x, s = _c(x), _c(s)
+    P, HW = _planes(x)
+    _need(s, P, "scale_rows s")
+    _need(r, x.numel(), "scale_add r")
+    y = torch.empty_like(x)
+    check(LIB.ganamd_scale_add(ptr(x), ptr(s), ptr(None if r is None else _c(r)), P, HW, ptr(y), stream()),
+          "scale_add")
+    return y
+
+
+class ScaleRows(Function):
+    """y[c,b,:] = x[c,b,:] * s[c,b]   (any order of derivative, with PlaneDot)."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.save_for_backward(x, s)
+        return _scale_rows(x, s)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, s = ctx.saved_tensors
+        gx = ScaleRows.apply(g, s) if ctx.needs_input_grad[0] else None
+        gs = PlaneDot.apply(g, x) if ctx.needs_input_grad[1] else None
+        return gx, gs
+
+
+class PlaneDot(Function):
+    """z[c,b] = sum_hw a[c,b,:] * b[c,b,:]   (any order of derivative, with ScaleRows)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return plane_dot(a, b)
+
+    @staticmethod
+    def backward(ctx, gz):
+        a, b = ctx.saved_tensors
+        ga = ScaleRows.apply(b, gz) if ctx.needs_input_grad[0] else None
+        gb = ScaleRows.apply(a, gz) if ctx.needs_input_grad[1] else None
+        return ga, gb
+
+
+class ScaleAdd(Function):
+    """y = r + x * s[c,b]: the SE-gated residual of both networks (generator_13_5.py:455-466,
+    discriminator_9_4.py:158-161); differentiable to any order (the critic's GP)."""
+
+    @staticmethod
+    def forward(ctx, x, s, r):
+        ctx.save_for_backward(x, s)
+        return _scale_rows(x, s, r)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, s = ctx.saved_tensors
+        gx = ScaleRows.apply(g, s) if ctx.needs_input_grad[0] else None
+        gs = PlaneDot.apply(g, x) if ctx.needs_input_grad[1] else None
+        return gx, gs, g
+
+
+def scale_add(x, s, r):
+    return ScaleAdd.apply(x, s, r)
+
+
+class Mix(Function):
+    """y = sum_m att[m] * f_m   (selective-kernel mixing; generator only, first order)."""
+
+    @staticmethod
+    def forward(ctx, att, *feas):
+        feas = [_c(f) for f in feas]
+        att = _c(att)
+        M = len(feas)
+        P, HW = _planes(feas[0])
+        _need(att, M * P, "mix att")
+        y = torch.empty_like(feas[0])
+        fp = [ptr(f) for f in feas] + [None] * (4 - M)
+        check(LIB.ganamd_mix_fwd(M, *fp, ptr(att), P, HW, ptr(y), stream()), "mix_fwd")
+        ctx.save_for_backward(att, *feas)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        att, *feas = ctx.saved_tensors
+        gy = _c(gy)
+        M = len(feas)
+        P, HW = _planes(feas[0])
+        gfs = [torch.empty_like(f) if ctx.needs_input_grad[1 + i] else None for i, f in enumerate(feas)]
+        gatt = torch.empty_like(att) if ctx.needs_input_grad[0] else None
+        fp = [ptr(f) for f in feas] + [None] * (4 - M)
+        gp = [ptr(g) for g in gfs] + [None] * (4 - M)
+        check(LIB.ganamd_mix_bwd(M, *fp, ptr(att), P, HW, ptr(gy), *gp, ptr(gatt), stream()), "mix_bwd")
+        return (gatt, *gfs)
+
+
+def mix(feas, att):
+    """feas: M tensors [C,B,H,W]; att: [M,C,B]."""
+    return Mix.apply(att, *feas)
+
+
+class AddPReLU(Function):
+    """y = PReLU(a + b)   (generator only, first order)."""
+
+    @staticmethod
+    def forward(ctx, a, b, alpha):
+        a, b = _c(a), _c(b)
+        C, L = _rows(a)
+        _need(alpha, C, "add_prelu alpha")
+        y = torch.empty_like(a)
+        check(LIB.ganamd_add_prelu(ptr(a), ptr(b), ptr(alpha), C, L, ptr(y), stream()), "add_prelu")
+        ctx.save_for_backward(a, b, alpha)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        a, b, alpha = ctx.saved_tensors
+        z = a + b
+        C, L = _rows(z)
+        gz = torch.empty_like(z)
+        ga = torch.empty_like(alpha)
+        ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), z.device)
+        check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(z), ptr(alpha), C, L, ptr(gz), ptr(ga), ptr(ws), stream()),
+              "prelu_bwd")
+        return gz, gz, ga
+
+
+def add_prelu(a, b, alpha):
+    return AddPReLU.apply(a, b, alpha)
+
+
+def modconv_fused(x, s, d, w, geo, c, noise=None, noise_scale=None, act=None):
+    """No-grad modulated conv with the StyleConv noise and the following PReLU in the GEMM
+    epilogue (ganamd_conv_fwd_ex): y = PReLU(c*d*conv(x*s, W) + noise_scale*noise)."""
+    x, s, d = _c(x), _c(s), _c(d)
+    _need(d, geo.Cout * geo.B, "conv_fwd y_scale")
+    _need(x, geo.Cin * geo.B * geo.H * geo.W, "conv_fwd x")
+    _need(s, geo.Cin * geo.B, "conv_fwd x_scale")
+    _need(noise, geo.Cout * geo.B * geo.OH * geo.OW, "conv_fwd noise")
+    _need(noise_scale, geo.Cout if noise is not None else None, "conv_fwd noise_scale")
+    _need(act, geo.Cout, "conv_fwd act")
+    return _conv_fwd_ex(geo, x, w, s, d, c, noise, noise_scale, act)
+
+
+def _conv_fwd_ex(geo, x, w, xs, ys, alpha, noise=None, noise_scale=None, act=None):
+    FlopCounter.add(geo, "fwd", xs is not None, ys is not None)
+    y = torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device, dtype=torch.float32)
+    pw = PackCache.get(geo, _lib.CONV_FWD, w)
+    packed = pw is not None
+    nb = geo.ws_bytes(_lib.CONV_FWD, packed)
+    ws = workspace(nb, x.device) if nb else None
+    check(LIB.ganamd_conv_fwd_ex(geo.desc(packed), ptr(x), ptr(pw if packed else _c(w)), None, ptr(xs), ptr(ys),
+                                 float(alpha), ptr(None if noise is None else _c(noise)), ptr(noise_scale),
+                                 ptr(act), ptr(y), ptr(ws), stream()), "conv_fwd_ex")
+    return y
 
 
 # ------------------------------------------------------------------------------------------

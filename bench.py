@@ -218,7 +218,33 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             parts[name] = round(e0.elapsed_time(e1), 1)
-        print(f"[bench] ms per graph: {parts}", file=sys.stderr, flush=True)
+        # eager pieces of the critic step (indicative; eager adds launch gaps)
+        def timed(fn, n=2):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return round(e0.elapsed_time(e1) / n, 1)
+
+        z = torch.randn(B, 256, 1, 1, device=dev)
+        x2 = torch.randn(2 * B, 3, 64, 64, device=dev)
+
+        def g_fwd():
+            with torch.no_grad():
+                G(z)
+
+        def d_fwd_bwd():
+            D(x2, segments=2).sum().backward()
+
+        def gp():
+            (10 * tr.gradient_penalty(x2[:B], x2[B:], B)).backward()
+
+        parts.update(eager_g_forward=timed(g_fwd), eager_d_fwd_bwd_2B=timed(d_fwd_bwd), eager_gp=timed(gp))
+        print(f"[bench] ms per graph / piece: {parts}", file=sys.stderr, flush=True)
     if rank == 0:
         print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
               f"issued GEMM launches/iter {ops.FlopCounter.launches}", file=sys.stderr, flush=True)

@@ -75,6 +75,16 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
                     hipStream_t stream);
 
+/* ganamd_conv_fwd with an extended epilogue, applied after bias in this order:
+ *   y += noise_scale[co] * noise[co][b,oh,ow]      (StyleConv noise, generator_13_5.py:263-266)
+ *   y  = PReLU(y; act_alpha[co])                    (the PReLU that follows a StyleConv)
+ * noise / act_alpha may be NULL.  Used by the generator's no-grad forward (the critic step's
+ * fake batch), where no pre-activation needs to be kept. */
+int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
+                       const float* x_scale, const float* y_scale, float alpha, const float* noise,
+                       const float* noise_scale, const float* act_alpha, float* y, void* workspace,
+                       hipStream_t stream);
+
 /* gx = alpha * dConv/dx applied to (gy * gy_scale[co][b]), including the ReplicationPad2d
  * backward (edge folding).  Replaces aten convolution_backward (input grad) + replication_pad2d_backward.
  * Workspace: ganamd_conv_workspace(d, GANAMD_CONV_DGRAD). */
@@ -177,6 +187,24 @@ typedef struct ganamd_gtile {
 
 int ganamd_grouped_gemm(const float* A, const float* B, float* C, const float* bias, const ganamd_gtile* tiles,
                         int n_tiles, int a_trans, int b_trans, int b_square, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused per-plane elementwise ops (CNHW: planes = C*B planes of HW floats; per-(c,b)
+ * coefficients [C][B] are indexed by plane).
+ * ------------------------------------------------------------------------------------- */
+/* y = sum_{m<M} att[m][plane] * f_m   (M <= 4; SK mixing, generator_13_5.py:80-89,165-170,196-202) */
+int ganamd_mix_fwd(int M, const float* f0, const float* f1, const float* f2, const float* f3, const float* att,
+                   long planes, long HW, float* y, hipStream_t stream);
+/* gf_m = gy * att[m] (gf_m may be NULL), gatt[m][plane] = sum_hw gy * f_m (gatt may be NULL) */
+int ganamd_mix_bwd(int M, const float* f0, const float* f1, const float* f2, const float* f3, const float* att,
+                   long planes, long HW, const float* gy, float* gf0, float* gf1, float* gf2, float* gf3, float* gatt,
+                   hipStream_t stream);
+/* y[c][l] = PReLU(a + b; alpha[c])   (ResnetInit, generator_13_5.py:343-349) */
+int ganamd_add_prelu(const float* a, const float* b, const float* alpha, int C, long L, float* y, hipStream_t stream);
+/* y = r + x * s[plane]  (r may be NULL: y = x * s)   (SE gating + residual, generator_13_5.py:455-466,
+ * discriminator_9_4.py:158-161) */
+int ganamd_scale_add(const float* x, const float* s, const float* r, long planes, long HW, float* y,
+                     hipStream_t stream);
 
 /* Library identification (for load checks). */
 const char* ganamd_version(void);

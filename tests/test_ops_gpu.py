@@ -49,6 +49,11 @@ CONV_CASES = [
     (8, 3, 64, 64, 3, 1, 1, 1),
     (4, 96, 32, 96, 5, 1, 2, 1),
     (4, 1025, 4, 1025, 3, 1, 1, 1),
+    # small maps take the scatter-form dgrad (GEMM over output pixels + fold): edges on both sides
+    (4, 20, 2, 24, 3, 1, 1, 1),
+    (4, 8, 1, 8, 3, 1, 1, 1),
+    (4, 12, 4, 12, 3, 1, 1, 0),
+    (2, 6, 7, 5, 5, 1, 2, 1),
 ]
 
 
@@ -376,3 +381,81 @@ def test_packed_weight_cache_tracks_updates(ops):
     opt.step()
     assert rel(run(), fresh()) == 0
     assert rel(run(), y1) > 1e-3
+
+
+@pytest.mark.parametrize("M,H", [(2, 8), (2, 5), (3, 4), (1, 16)])
+def test_mix_fwd_bwd(ops, M, H):
+    g = torch.Generator().manual_seed(M * 10 + H)
+    C, B = 6, 4
+    feas = [torch.randn(C, B, H, H, generator=g, dtype=torch.float64, requires_grad=True) for _ in range(M)]
+    att = torch.rand(M, C, B, generator=g, dtype=torch.float64, requires_grad=True)
+    ref = sum(f * att[m][:, :, None, None] for m, f in enumerate(feas))
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    want = torch.autograd.grad(ref, feas + [att], gy)
+    fg = [f.detach().float().cuda().requires_grad_() for f in feas]
+    ag = att.detach().float().cuda().requires_grad_()
+    y = ops.mix(fg, ag)
+    got = torch.autograd.grad(y, fg + [ag], gy.float().cuda())
+    assert rel(y, ref) < 1e-6
+    for a, b in zip(got, want):
+        assert rel(a, b) < 1e-5
+
+
+def test_add_prelu_fwd_bwd(ops):
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(5, 4, 6, 6, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(5, 4, 6, 6, generator=g, dtype=torch.float64, requires_grad=True)
+    al = torch.rand(5, generator=g, dtype=torch.float64, requires_grad=True)
+    z = a + b
+    ref = torch.where(z > 0, z, al[:, None, None, None] * z)
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    want = torch.autograd.grad(ref, (a, b, al), gy)
+    ins = [t.detach().float().cuda().requires_grad_() for t in (a, b, al)]
+    y = ops.add_prelu(*ins)
+    got = torch.autograd.grad(y, ins, gy.float().cuda())
+    assert rel(y, ref) < 1e-6
+    for x, w in zip(got, want):
+        assert rel(x, w) < 1e-5
+
+
+def test_scale_add_double_backward(ops):
+    """ScaleAdd / ScaleRows / PlaneDot are closed under differentiation (the critic's GP)."""
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 4, 5, 5, generator=g, dtype=torch.float64, requires_grad=True)
+    s = torch.rand(3, 4, generator=g, dtype=torch.float64, requires_grad=True)
+    r = torch.randn(3, 4, 5, 5, generator=g, dtype=torch.float64, requires_grad=True)
+    v = torch.randn(3, 4, 5, 5, generator=g, dtype=torch.float64)
+
+    def loss(f, xx, ss, rr):
+        y = f(xx, ss, rr)
+        gx, gs = torch.autograd.grad((y * y * v.to(y)).sum(), (xx, ss), create_graph=True)
+        return (gx.pow(2).sum() + gs.pow(3).sum())
+
+    ref = loss(lambda a, b, c: c + a * b[:, :, None, None], x, s, r)
+    want = torch.autograd.grad(ref, (x, s, r))
+    ins = [t.detach().float().cuda().requires_grad_() for t in (x, s, r)]
+    out = loss(ops.scale_add, *ins)
+    got = torch.autograd.grad(out, ins)
+    assert abs(float(out) - float(ref)) / abs(float(ref)) < 1e-5
+    for a, b in zip(got, want):
+        assert rel(a, b) < 1e-4
+
+
+def test_conv_fwd_ex_noise_act(ops):
+    g = torch.Generator().manual_seed(5)
+    B, Cin, Cout, H, k = 4, 12, 10, 8, 3
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64)
+    sx = torch.rand(Cin, B, generator=g, dtype=torch.float64) + 0.5
+    sy = torch.rand(Cout, B, generator=g, dtype=torch.float64) + 0.5
+    nz = torch.randn(Cout, B, H, H, generator=g, dtype=torch.float64)
+    ns = torch.rand(Cout, generator=g, dtype=torch.float64)
+    al = torch.rand(Cout, generator=g, dtype=torch.float64)
+    xm = x * sx.t()[:, :, None, None]
+    y = ref_conv(xm, w * 0.3, None, k, 1, 1, 1) * sy.t()[:, :, None, None]
+    y = y + ns[None, :, None, None] * nz.permute(1, 0, 2, 3)
+    y = torch.where(y > 0, y, al[None, :, None, None] * y)
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, 1)
+    got = ops.modconv_fused(cn(x), sx.float().cuda(), sy.float().cuda(), w.float().cuda(), geo, 0.3,
+                            nz.float().cuda(), ns.float().cuda(), al.float().cuda())
+    assert rel(nc(got), y) < 1e-5
