@@ -95,6 +95,47 @@ def cpu_baseline(threads):
                       f"{t2 - t1:.2f}s, t_iter = 5*t_D + t_G = {t_iter:.1f}s; nproc={os.cpu_count()}"}
 
 
+# Dominant kernel: the implicit-GEMM conv kernel (conv_gemm_kernel, all instances ~55 % of the
+# iteration's GPU time; profiles/).  Representative launch: the critic's mid-level block conv in
+# the real+fake pass -- D9_4 128->128 channels, 3x3 replication pad, 32x32, B = 128 -- one
+# conv_gemm_kernel<128,128,2,2,1,false> launch per call (1024 tiles, no split-K).
+PROBE = dict(B=128, cin=128, h=32, cout=128, k=3)
+
+
+def roofline_probe(dev, reps=20):
+    import gan_amd.ops as ops
+    g = ops.conv_geo(PROBE["B"], PROBE["cin"], PROBE["h"], PROBE["h"], PROBE["cout"], PROBE["k"], 1, 1)
+    x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
+    w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
+    with torch.no_grad():
+        for _ in range(3):
+            ops._conv_fwd(g, x, w, None, None, None, 0.03)   # packs the weight once (ops.PackCache)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    with torch.no_grad():
+        for _ in range(reps):
+            ops._conv_fwd(g, x, w, None, None, None, 0.03)
+    e1.record(s)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    flop = 2.0 * g.B * g.OH * g.OW * g.Cout * g.Cin * g.K * g.K
+    tf = flop / us / 1e6
+    out = {"bound": "mfma", "kernel": "conv_gemm_kernel<128,128,2,2,1,false>",
+           "shape": "conv fwd B=128 128->128 3x3 replicate-pad 32x32 (D9_4 block conv, critic real+fake pass)",
+           "algorithmic_gflop_per_launch": flop / 1e9, "launch_us": us,
+           "achieved": tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP32_MFMA_PEAK_TFLOPS,
+           "traffic": None}
+    # HBM bytes per launch from rocprofv3 PMC passes of this launch (tools/pmc_traffic.sh), if recorded
+    tfile = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "roofline_traffic.json")
+    if os.path.exists(tfile):
+        t = json.load(open(tfile))
+        out["traffic"] = t.get("bytes_per_launch")
+        out["traffic_source"] = t.get("source")
+    return out
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args.gpus, args.backend)
@@ -245,6 +286,9 @@ def main():
 
         parts.update(eager_g_forward=timed(g_fwd), eager_d_fwd_bwd_2B=timed(d_fwd_bwd), eager_gp=timed(gp))
         print(f"[bench] ms per graph / piece: {parts}", file=sys.stderr, flush=True)
+    probe = None
+    if rank == 0 and world == 1:
+        probe = roofline_probe(dev)
     if rank == 0:
         print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
               f"issued GEMM launches/iter {ops.FlopCounter.launches}", file=sys.stderr, flush=True)
@@ -267,11 +311,11 @@ def main():
             "config": {"workload": "G13_5+D9_4 WGAN-GP iteration (5 critic steps with GP + 1 generator step), "
                                    "64x64x3", "global_batch": B * world, "per_gpu_batch": B, "n_critic": N_CRITIC,
                        "parallelism": f"dp{world}", "mode": args.mode},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "conv_gemm/wgrad_gemm implicit-GEMM family (99% of algorithmic FLOPs)",
-                         "algorithmic_gflop_per_iter": ALGO_GFLOP_PER_IMAGE * B,
-                         "issued_gemm_gflop_per_iter": issued_flops / 1e9},
+            "roofline": dict(probe or {}, **{
+                # whole iteration: algorithmic FLOPs / iteration time, per GPU
+                "iteration_tflops": achieved, "iteration_frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                "algorithmic_gflop_per_iter": ALGO_GFLOP_PER_IMAGE * B,
+                "issued_gemm_gflop_per_iter": issued_flops / 1e9}),
             "wall_s": wall,
         }
         if world == 1 and not args.no_cpu_baseline:

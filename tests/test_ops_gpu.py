@@ -436,7 +436,7 @@ def test_scale_add_double_backward(ops):
     ins = [t.detach().float().cuda().requires_grad_() for t in (x, s, r)]
     out = loss(ops.scale_add, *ins)
     got = torch.autograd.grad(out, ins)
-    assert abs(float(out) - float(ref)) / abs(float(ref)) < 1e-5
+    assert abs(float(out.detach()) - float(ref.detach())) / abs(float(ref.detach())) < 1e-5
     for a, b in zip(got, want):
         assert rel(a, b) < 1e-4
 

@@ -1,0 +1,26 @@
+#!/bin/bash
+# The round's committed evidence: the bench line, a rocprofv3 kernel-trace/stats run of the SAME
+# bench command (summaries only leave /tmp), the roofline-probe launches' average from that trace,
+# and the PMC traffic of the probe launch.   usage: tools/round_profile.sh rNN
+set -e
+R=$1
+export TMPDIR=/tmp
+timeout -k 10 300 tools/pmc_traffic.sh > gpurun_out/${R}_pmc_traffic.log 2>&1
+cp gpurun_out/roofline_traffic.json profiles/roofline_traffic.json
+rm -rf /tmp/prof_$R
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/prof_$R -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/${R}_bench_prof.log 2>&1
+T=$(find /tmp/prof_$R -name "*kernel_trace.csv")
+S=$(find /tmp/prof_$R -name "*kernel_stats.csv")
+cp "$S" gpurun_out/${R}_bench_kernel_stats.csv
+MS=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]['ms_per_step'])" gpurun_out/${R}_bench_prof.log)
+python3 tools/trace_summary.py "$T" --last $(python3 -c "print($MS/1000*0.98)") --top 60 > gpurun_out/${R}_iteration_summary.txt || true
+python3 - "$T" > gpurun_out/${R}_roofline_probe.txt <<'PY'
+import csv, sys
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_gemm_kernel<128, 128, 2, 2, 1, false>" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+last = rows[-20:]
+d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
+print(f"roofline probe: last {len(d)} dispatches of conv_gemm_kernel<128,128,2,2,1,false> in the bench trace")
+print(f"average {sum(d) / len(d):.1f} us  min {min(d):.1f}  max {max(d):.1f}")
+PY
+timeout -k 10 900 python3 bench.py > gpurun_out/${R}_bench.log 2>&1
