@@ -573,12 +573,8 @@ int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
-int conv_block_target() {
-  static const int v = env_int("GANAMD_CONV_BLOCKS", 1024);
-  return v;
-}
-int wgrad_block_target() {
-  static const int v = env_int("GANAMD_WGRAD_BLOCKS", 1024);
+int splitk_enabled() {   // GANAMD_SPLITK=0 disables split-K (experiments)
+  static const int v = env_int("GANAMD_SPLITK", 1);
   return v;
 }
 
@@ -592,30 +588,47 @@ struct Plan {
 };
 
 int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
-int conv_wide_min_n() {
-  static const int v = env_int("GANAMD_CONV_WIDE", 0);   // N at/above which 256-wide tiles are used (0: never)
-  return v;
-}
-int conv_bn(int bm, int N) { return (bm == 32 || (conv_wide_min_n() > 0 && N >= conv_wide_min_n())) ? 256 : 128; }
+int conv_bn(int bm, int) { return bm == 32 ? 256 : 128; }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
 
-Plan split_plan(int bm, int bn, int tiles, int kt_total, int target, int max_splits) {
-  int splits = 1;
-  // split K while the grid is short of `target` workgroups, keeping >= 4 K-steps per split; a GEMM
-  // whose whole loop is tiny (tiles * K-steps < 256) is launch-bound and is left alone
-  const long work = (long)tiles * kt_total;
-  if (tiles < target && kt_total >= 8 && work >= 256)
-    splits = std::min((target + tiles - 1) / tiles, std::max(1, kt_total / 4));
-  splits = std::min(splits, max_splits);
-  const int per = (kt_total + splits - 1) / splits;
-  splits = (kt_total + per - 1) / per;
-  return Plan{bm, bn, splits, per};
+// Split-K by a small cost model: a GEMM of `tiles` output tiles, each `kt_total` K-steps of
+// `kflop` FLOPs, runs in ceil(tiles*s / slots) waves of blocks (slots = resident blocks per CU
+// x 256 CUs, from the compiler's resource report of the instance) of ceil(kt_total/s) K-steps;
+// splitting adds the slab round trip and a reduce launch.  Pure function of the geometry (the
+// workspace query and the launch agree).
+constexpr int kCUs = 256;
+constexpr double kBlockTflops = 110.0;   // measured sustained fp32 MFMA rate of the GEMM kernels
+
+Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_elems, int occ, int max_splits,
+                int min_k) {
+  const int slots = occ * kCUs;
+  const double t_k = kflop / (kBlockTflops * 1e12 / slots) * 1e6;   // us per K-step of one block
+  auto cost = [&](int s) {
+    const long per = (kt_total + s - 1) / s;
+    const long waves = ((long)tiles * s + slots - 1) / slots;
+    double c = (double)waves * per * t_k;
+    if (s > 1) c += 3.0 + (2.0 * s + 1.0) * out_elems * 4.0 / 4e12 * 1e6;
+    return c;
+  };
+  int best = 1;
+  double bc = cost(1);
+  if (splitk_enabled())
+    for (int s = 2; s <= max_splits && kt_total / s >= min_k; ++s) {
+      const double c = cost(s);
+      if (c < bc * 0.97) {   // split only for a clear win
+        bc = c;
+        best = s;
+      }
+    }
+  const int per = (kt_total + best - 1) / best;
+  return Plan{bm, bn, (kt_total + per - 1) / per, per};
 }
 
 Plan conv_plan(int M, int N, int Ck, int T) {
   const int bm = conv_bm(M), bn = conv_bn(bm, N);
   const int tiles = ((N + bn - 1) / bn) * ((M + bm - 1) / bm);
-  return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, conv_block_target(), 16);
+  const int occ = bm == 64 ? 5 : 3;
+  return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, 2.0 * bm * bn * BK, (long)M * N, occ, 16, 4);
 }
 
 // bytes of the packed A operand of a conv GEMM (rows padded to the tile, K to whole K-steps)
@@ -632,7 +645,8 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
     bn = 64;
   }
   const int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
-  return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, wgrad_block_target(), 256);
+  const int occ = bn == 64 ? 4 : (bm >= 96 ? 2 : 3);
+  return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, 2.0 * bm * bn * BKW, (long)M * J * T, occ, 256, 4);
 }
 
 __global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int N, int ohw, int B,
@@ -678,15 +692,8 @@ hipError_t launch_conv(ConvArgs p, const Plan& pl, float* slab, hipStream_t st) 
 
 template <int MODE, bool BSCALE>
 hipError_t dispatch_conv_tile(const ConvArgs& p, const Plan& pl, float* slab, hipStream_t st) {
-  if (pl.bn == 256) {
-    switch (pl.bm) {
-      case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
-      case 64: return launch_conv<64, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
-      case 96: return launch_conv<96, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
-      default: return launch_conv<128, 256, 2, 2, MODE, BSCALE>(p, pl, slab, st);
-    }
-  }
   switch (pl.bm) {
+    case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
     case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE>(p, pl, slab, st);
     default: return launch_conv<128, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);

@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--mode", choices=["eager", "graph"], default="graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the post-run breakdown and roofline probe (clean traces of the timed region)")
     ap.add_argument("--no-bank", action="store_true", help="per-module style MLPs (A/B against the style bank)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
     return ap.parse_args()
@@ -249,7 +251,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     secs = float(t)
 
-    if rank == 0 and args.mode == "graph" and world == 1:
+    if rank == 0 and args.mode == "graph" and world == 1 and not args.no_extras:
         # breakdown (outside the timed region): one critic-step graph, one generator-step graph
         parts = {}
         for name, g in (("critic_step", gd), ("generator_step", gg)):
@@ -287,7 +289,7 @@ def main():
         parts.update(eager_g_forward=timed(g_fwd), eager_d_fwd_bwd_2B=timed(d_fwd_bwd), eager_gp=timed(gp))
         print(f"[bench] ms per graph / piece: {parts}", file=sys.stderr, flush=True)
     probe = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_extras:
         probe = roofline_probe(dev)
     if rank == 0:
         print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "

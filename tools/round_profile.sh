@@ -13,7 +13,13 @@ T=$(find /tmp/prof_$R -name "*kernel_trace.csv")
 S=$(find /tmp/prof_$R -name "*kernel_stats.csv")
 cp "$S" gpurun_out/${R}_bench_kernel_stats.csv
 MS=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]['ms_per_step'])" gpurun_out/${R}_bench_prof.log)
-python3 tools/trace_summary.py "$T" --last $(python3 -c "print($MS/1000*0.98)") --top 60 > gpurun_out/${R}_iteration_summary.txt || true
+# the per-iteration breakdown comes from a second trace without the post-run extras (its last
+# ms_per_step window is exactly the final timed iteration)
+rm -rf /tmp/prof_${R}b
+timeout -k 10 900 rocprofv3 --kernel-trace -d /tmp/prof_${R}b -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extras > gpurun_out/${R}_bench_prof2.log 2>&1
+T2=$(find /tmp/prof_${R}b -name "*kernel_trace.csv")
+MS2=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]['ms_per_step'])" gpurun_out/${R}_bench_prof2.log)
+python3 tools/trace_summary.py "$T2" --last $(python3 -c "print($MS2/1000*0.98)") --top 60 > gpurun_out/${R}_iteration_summary.txt
 python3 - "$T" > gpurun_out/${R}_roofline_probe.txt <<'PY'
 import csv, sys
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_gemm_kernel<128, 128, 2, 2, 1, false>" in r["Kernel_Name"]]
