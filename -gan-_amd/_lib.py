@@ -54,13 +54,13 @@ _SIGS = {
     "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
     "ganamd_rowreduce_workspace": (c_size_t, [c_int, c_long]),
     "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, vp]),
-    "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp]),
     "ganamd_prelu_fwd": (c_int, [vp, vp, c_int, c_long, vp, vp]),
-    "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, vp, vp]),
+    "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),
     "ganamd_prelu_bwd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_long, vp, vp, vp, vp, vp]),
     "ganamd_resample2d": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int, vp]),
     "ganamd_plane_dot": (c_int, [vp, vp, c_long, c_long, c_float, vp, vp]),
-    "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, vp, vp]),
+    "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, c_int, vp, vp]),
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),
     "ganamd_adamw": (c_int, [vp, vp, vp, vp, c_long, vp, c_float, c_float, c_float, c_float, c_float, vp]),
     "ganamd_grouped_gemm": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp]),

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(kNT) void bn_small_bwd_kernel(const float* __restri
                                                            const float* __restrict__ beta,
                                                            const float* __restrict__ alpha, float* __restrict__ gx,
                                                            float* __restrict__ ggamma, float* __restrict__ gbeta,
-                                                           float* __restrict__ galpha) {
+                                                           float* __restrict__ galpha, int accumulate) {
   const int c = blockIdx.x * (kNT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= C) return;
   const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
@@ -214,9 +214,9 @@ __global__ __launch_bounds__(kNT) void bn_small_bwd_kernel(const float* __restri
   sgx = wave_sum_d(sgx);
   if (alpha) sa = wave_sum_d(sa);
   if (lane == 0) {
-    gbeta[c] = (float)sg;
-    ggamma[c] = (float)sgx;
-    if (alpha && galpha) galpha[c] = (float)sa;
+    gbeta[c] = accumulate ? gbeta[c] + (float)sg : (float)sg;
+    ggamma[c] = accumulate ? ggamma[c] + (float)sgx : (float)sgx;
+    if (alpha && galpha) galpha[c] = accumulate ? galpha[c] + (float)sa : (float)sa;
   }
   const float mg = (float)(sg / L), mgx = (float)(sgx / L), k = ga * is;
   float* gxr = gx + (long)c * L;
@@ -281,7 +281,9 @@ __global__ __launch_bounds__(kNT) void bn_act_bwd_partial_kernel(
   }
 }
 
-__global__ void reduce3_kernel(const double* __restrict__ part, int C, int S, float* o0, float* o1, float* o2) {
+// o0..o2 (=|+=) the row sums; s0/s1 (optional) always receive the plain sums of rows 0/1
+__global__ void reduce3_kernel(const double* __restrict__ part, int C, int S, float* o0, float* o1, float* o2,
+                               int accumulate, float* s0, float* s1) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double* p = part + (long)c * S * 3;
@@ -291,9 +293,11 @@ __global__ void reduce3_kernel(const double* __restrict__ part, int C, int S, fl
     b += p[3 * s + 1];
     d += p[3 * s + 2];
   }
-  if (o0) o0[c] = (float)a;
-  if (o1) o1[c] = (float)b;
-  if (o2) o2[c] = (float)d;
+  if (s0) s0[c] = (float)a;
+  if (s1) s1[c] = (float)b;
+  if (o0) o0[c] = accumulate ? o0[c] + (float)a : (float)a;
+  if (o1) o1[c] = accumulate ? o1[c] + (float)b : (float)b;
+  if (o2) o2[c] = accumulate ? o2[c] + (float)d : (float)d;
 }
 
 // gx = gamma*invstd*(g - sum(g)/L - xhat*sum(g*xhat)/L); the partial sums were reduced into
@@ -387,12 +391,12 @@ __global__ __launch_bounds__(kNT) void prelu_bwd_bwd_kernel(const float* __restr
   }
 }
 
-__global__ void reduce1_kernel(const float* __restrict__ part, int C, int S, float* out) {
+__global__ void reduce1_kernel(const float* __restrict__ part, int C, int S, float* out, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float a = 0.f;
   for (int s = 0; s < S; ++s) a += part[(long)c * S + s];
-  out[c] = a;
+  out[c] = accumulate ? out[c] + a : a;
 }
 
 // ---------------------------------------------------------------- row / plane reductions
@@ -431,6 +435,28 @@ __global__ __launch_bounds__(kNT) void plane_dot_kernel(const float* __restrict_
     acc = wave_sum(acc);
     if (lane == 0) out[p] = scale * acc;
   }
+}
+
+// planes of >= 1024 floats: a 256-thread block per plane, 16-byte loads
+__global__ __launch_bounds__(kNT) void plane_dot_big_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                            long HW, float scale, float* __restrict__ out) {
+  __shared__ float sh[4];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const long p = blockIdx.x;
+  const f4* a4 = reinterpret_cast<const f4*>(a + p * HW);
+  const f4* b4 = b ? reinterpret_cast<const f4*>(b + p * HW) : nullptr;
+  float acc = 0.f;
+  for (long i = threadIdx.x; i < HW / 4; i += kNT) {
+    const f4 u = a4[i];
+    if (b4) {
+      const f4 v = b4[i];
+      acc += u[0] * v[0] + u[1] * v[1] + u[2] * v[2] + u[3] * v[3];
+    } else {
+      acc += u[0] + u[1] + u[2] + u[3];
+    }
+  }
+  acc = block_sum(acc, sh);
+  if (threadIdx.x == 0) out[p] = scale * acc;
 }
 
 __global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int T, float* __restrict__ out) {
@@ -517,7 +543,9 @@ extern "C" {
 
 const char* ganamd_version(void) { return "ganamd 0.1 gfx950"; }
 
-size_t ganamd_rowreduce_workspace(int C, long L) { return sizeof(double) * 3 * (size_t)C * splits_for(L); }
+size_t ganamd_rowreduce_workspace(int C, long L) {
+  return sizeof(double) * 3 * (size_t)C * splits_for(L) + 2 * sizeof(float) * (size_t)C;
+}
 
 int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
@@ -541,22 +569,23 @@ int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const f
 
 int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,
                       const float* alpha, const float* save_mean, const float* save_invstd, float* gx, float* ggamma,
-                      float* gbeta, float* galpha, void* workspace, hipStream_t st) {
+                      float* gbeta, float* galpha, int accumulate, void* workspace, hipStream_t st) {
   if (!gy || !x || !gamma || !beta || !save_mean || !save_invstd || !gx || !ggamma || !gbeta || !workspace)
     return GANAMD_EINVAL;
   if (L <= kSmallL) {
     hipLaunchKernelGGL(bn_small_bwd_kernel, dim3((C + 3) / 4), dim3(kNT), 0, st, gy, x, C, (int)L, save_mean,
-                       save_invstd, gamma, beta, alpha, gx, ggamma, gbeta, galpha);
+                       save_invstd, gamma, beta, alpha, gx, ggamma, gbeta, galpha, accumulate);
     return ok(hipGetLastError());
   }
   const int S = splits_for(L);
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_act_bwd_partial_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, L, S, save_mean, save_invstd,
                      gamma, beta, alpha, part);
+  float* sums = reinterpret_cast<float*>(part + (size_t)3 * C * S);   // plain sum(g), sum(g*xhat) for gx
   hipLaunchKernelGGL(reduce3_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, gbeta, ggamma,
-                     alpha ? galpha : nullptr);
+                     alpha ? galpha : nullptr, accumulate, sums, sums + C);
   hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, gy, x, C, L, save_mean,
-                     save_invstd, gamma, beta, alpha, gbeta, ggamma, gx);
+                     save_invstd, gamma, beta, alpha, sums, sums + C, gx);
   return ok(hipGetLastError());
 }
 
@@ -567,12 +596,13 @@ int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y
 }
 
 int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C, long L, float* gx, float* galpha,
-                     void* workspace, hipStream_t st) {
+                     int accumulate, void* workspace, hipStream_t st) {
   if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
   const int S = splits_for(L);
   float* part = galpha ? static_cast<float*>(workspace) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, alpha, L, S, gx, part);
-  if (galpha) hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha);
+  if (galpha)
+    hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, accumulate);
   return ok(hipGetLastError());
 }
 
@@ -583,7 +613,7 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
   float* part = galpha ? static_cast<float*>(workspace) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, ggx, ggalpha, gy, x, alpha, L, S, ggy, gx,
                      part);
-  if (galpha) hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha);
+  if (galpha) hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, 0);
   return ok(hipGetLastError());
 }
 
@@ -605,16 +635,23 @@ int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float
   if (!a || !out || planes <= 0 || HW <= 0) return GANAMD_EINVAL;
   const long waves = planes;
   int blocks = (int)std::min<long>((waves + 3) / 4, 16384);
+  const bool big = HW >= 1024 && (HW % 4) == 0 && (reinterpret_cast<uintptr_t>(a) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(b) & 15) == 0;
+  if (big) {
+    hipLaunchKernelGGL(plane_dot_big_kernel, dim3((unsigned)planes), dim3(kNT), 0, st, a, b, HW, scale, out);
+    return ok(hipGetLastError());
+  }
   hipLaunchKernelGGL(plane_dot_kernel, dim3(blocks), dim3(kNT), 0, st, a, b, planes, HW, scale, out);
   return ok(hipGetLastError());
 }
 
-int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, void* workspace, hipStream_t st) {
+int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, int accumulate, void* workspace,
+                   hipStream_t st) {
   if (!a || !out || !workspace || C <= 0 || L <= 0) return GANAMD_EINVAL;
   const int S = splits_for(L);
   float* part = static_cast<float*>(workspace);
   hipLaunchKernelGGL(row_dot_kernel, dim3(S, C), dim3(kNT), 0, st, a, b, L, S, part);
-  hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, out);
+  hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, out, accumulate);
   return ok(hipGetLastError());
 }
 

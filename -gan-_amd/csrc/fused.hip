@@ -59,7 +59,8 @@ __global__ __launch_bounds__(kNT) void mix_fwd_kernel(Ptr4 f, const float* __res
   }
 }
 
-// one wave per plane: gf_m = g * att[m], gatt[m] = sum g * f_m
+// gf_m = g * att[m], gatt[m] = sum g * f_m.  Small planes: one wave per plane.  Planes of >= 1024
+// floats: one 256-thread block per plane with 16-byte accesses.
 template <int M>
 __global__ __launch_bounds__(kNT) void mix_bwd_kernel(Ptr4 f, const float* __restrict__ att, long planes, long HW,
                                                       const float* __restrict__ g, MPtr4 gf, float* __restrict__ gatt) {
@@ -87,6 +88,42 @@ __global__ __launch_bounds__(kNT) void mix_bwd_kernel(Ptr4 f, const float* __res
       const float d = wave_sum(dot[m]);
       if (lane == 0 && gatt) gatt[m * planes + p] = d;
     }
+  }
+}
+
+template <int M>
+__global__ __launch_bounds__(kNT) void mix_bwd_plane_kernel(Ptr4 f, const float* __restrict__ att, long planes,
+                                                            long HW, const float* __restrict__ g, MPtr4 gf,
+                                                            float* __restrict__ gatt) {
+  __shared__ float sh[M][4];
+  const long p = blockIdx.x;
+  const long base4 = p * HW / 4, n4 = HW / 4;
+  float a[M], dot[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    a[m] = att[m * planes + p];
+    dot[m] = 0.f;
+  }
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(g) + base4;
+  for (long i = threadIdx.x; i < n4; i += kNT) {
+    const f32x4 gv = g4[i];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (gf.p[m]) reinterpret_cast<f32x4*>(gf.p[m])[base4 + i] = gv * a[m];
+      const f32x4 fv = reinterpret_cast<const f32x4*>(f.p[m])[base4 + i];
+      dot[m] += gv[0] * fv[0] + gv[1] * fv[1] + gv[2] * fv[2] + gv[3] * fv[3];
+    }
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float d = wave_sum(dot[m]);
+    if (lane == 0) sh[m][w] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x < M && gatt) {
+    const int m = threadIdx.x;
+    gatt[m * planes + p] = sh[m][0] + sh[m][1] + sh[m][2] + sh[m][3];
   }
 }
 
@@ -137,6 +174,13 @@ void launch_mix_fwd(const Ptr4& f, const float* att, long planes, long HW, float
 template <int M>
 void launch_mix_bwd(const Ptr4& f, const float* att, long planes, long HW, const float* g, const MPtr4& gf,
                     float* gatt, hipStream_t st) {
+  bool vec = HW >= 1024 && (HW % 4) == 0 && aligned16(g);
+  for (int m = 0; m < M; ++m) vec = vec && aligned16(f.p[m]) && aligned16(gf.p[m]);
+  if (vec) {
+    hipLaunchKernelGGL((mix_bwd_plane_kernel<M>), dim3((unsigned)planes), dim3(kNT), 0, st, f, att, planes, HW, g,
+                       gf, gatt);
+    return;
+  }
   const int blocks = (int)std::min<long>((planes + 3) / 4, 16384);
   hipLaunchKernelGGL((mix_bwd_kernel<M>), dim3(blocks), dim3(kNT), 0, st, f, att, planes, HW, g, gf, gatt);
 }

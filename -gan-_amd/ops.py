@@ -218,11 +218,38 @@ def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
+def flat_grad(p):
+    """During a FIRST-order backward, the pre-bound flat-buffer gradient of parameter ``p`` (or of
+    the Parameter a view ``p`` comes from): the backward then accumulates into it with its own
+    kernel and returns None to autograd -- no per-parameter AccumulateGrad add launch (10k of them
+    per generator step otherwise).  None when autograd has to handle it (create_graph backward,
+    parameters outside an optimizer's flat buffer, plain tensors)."""
+    if p is None or torch.is_grad_enabled():
+        return None
+    root = p if p._base is None else p._base
+    if not isinstance(root, torch.nn.Parameter) or getattr(root, "_gan_flat", None) is None:
+        return None
+    g = root.grad
+    if g is None or not g.is_contiguous() or g.numel() != p.numel():
+        return None
+    return g
+
+
+def row_sum_acc(a, out):
+    """out[c] += sum over the row c of a (a conv bias gradient into the flat gradient buffer)."""
+    a = _c(a)
+    C, L = _rows(a)
+    _need(out, C, "row_sum out")
+    ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), a.device)
+    check(LIB.ganamd_row_dot(ptr(a), None, C, L, ptr(out), 1, ptr(ws), stream()), "row_dot")
+
+
 class ConvFwd(Function):
     """y = alpha * conv(x, w) + bias   (any order of derivative)."""
 
     @staticmethod
     def forward(ctx, x, w, bias, geo, alpha):
+        ctx.w_arg, ctx.b_arg = w, bias
         x, w = _c(x), _c(w)
         ctx.save_for_backward(x, w)
         ctx.geo, ctx.alpha, ctx.has_bias = geo, alpha, bias is not None
@@ -232,9 +259,21 @@ class ConvFwd(Function):
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         geo, alpha = ctx.geo, ctx.alpha
-        gx = ConvDgrad.apply(gy, w, geo, alpha) if ctx.needs_input_grad[0] else None
-        gw = ConvWgrad.apply(x, gy, geo, alpha) if ctx.needs_input_grad[1] else None
-        gb = gy.sum(dim=(1, 2, 3)) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        wv = ctx.w_arg if ctx.w_arg.is_contiguous() else w     # the Parameter itself where possible
+        gx = ConvDgrad.apply(gy, wv, geo, alpha) if ctx.needs_input_grad[0] else None
+        gw = gb = None
+        if ctx.needs_input_grad[1]:
+            tgt = flat_grad(ctx.w_arg)
+            if tgt is not None:
+                _conv_wgrad(geo, x, _c(gy), alpha=alpha, out=tgt, accumulate=True)
+            else:
+                gw = ConvWgrad.apply(x, gy, geo, alpha)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            tgt = flat_grad(ctx.b_arg)
+            if tgt is not None:
+                row_sum_acc(gy, tgt)
+            else:
+                gb = gy.sum(dim=(1, 2, 3))
         return gx, gw, gb, None, None
 
 
@@ -243,6 +282,7 @@ class ConvDgrad(Function):
 
     @staticmethod
     def forward(ctx, gy, w, geo, alpha):
+        ctx.w_arg = w
         gy, w = _c(gy), _c(w)
         ctx.save_for_backward(gy, w)
         ctx.geo, ctx.alpha = geo, alpha
@@ -253,7 +293,13 @@ class ConvDgrad(Function):
         gy, w = ctx.saved_tensors
         geo, alpha = ctx.geo, ctx.alpha
         g_gy = ConvFwd.apply(ggx, w, None, geo, alpha) if ctx.needs_input_grad[0] else None
-        g_w = ConvWgrad.apply(ggx, gy, geo, alpha) if ctx.needs_input_grad[1] else None
+        g_w = None
+        if ctx.needs_input_grad[1]:
+            tgt = flat_grad(ctx.w_arg)
+            if tgt is not None:
+                _conv_wgrad(geo, _c(ggx), gy, alpha=alpha, out=tgt, accumulate=True)
+            else:
+                g_w = ConvWgrad.apply(ggx, gy, geo, alpha)
         return g_gy, g_w, None, None
 
 
@@ -301,6 +347,7 @@ def _rows(x):
 class PReLU(Function):
     @staticmethod
     def forward(ctx, x, a):
+        ctx.a_arg = a
         x = _c(x)
         C, L = _rows(x)
         _need(a, C, "prelu alpha")
@@ -312,19 +359,29 @@ class PReLU(Function):
     @staticmethod
     def backward(ctx, gy):
         x, a = ctx.saved_tensors
-        gx, ga = PReLUBackward.apply(gy, x, a)
+        tgt = flat_grad(ctx.a_arg) if ctx.needs_input_grad[1] else None
+        if tgt is not None:   # first order: the slope gradient goes straight into the flat buffer
+            C, L = _rows(x)
+            gx = torch.empty_like(x)
+            ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
+            check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(x), ptr(a), C, L, ptr(gx), ptr(tgt), 1, ptr(ws), stream()),
+                  "prelu_bwd")
+            return gx, None
+        gx, ga = PReLUBackward.apply(gy, x, ctx.a_arg if ctx.a_arg.is_contiguous() else a)
         return gx, ga
 
 
 class PReLUBackward(Function):
     @staticmethod
     def forward(ctx, gy, x, a):
+        ctx.a_arg = a
         gy = _c(gy)
         C, L = _rows(x)
         gx = torch.empty_like(x)
         ga = torch.empty_like(a)
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
-        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), ptr(ga), ptr(ws), stream()), "prelu_bwd")
+        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), ptr(ga), 0, ptr(ws), stream()),
+              "prelu_bwd")
         ctx.save_for_backward(gy, x, a)
         return gx, ga
 
@@ -338,12 +395,16 @@ class PReLUBackward(Function):
         need_gy, need_x, need_a = ctx.needs_input_grad
         g_gy = torch.empty_like(x) if need_gy else None
         g_x = torch.empty_like(x) if (need_x and gga is not None) else None
+        tgt = flat_grad(ctx.a_arg) if need_a else None     # (once_differentiable: first order here)
         g_a = torch.empty_like(a) if need_a else None
         if g_gy is None and g_x is None and g_a is None:
             return None, None, None
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
         check(LIB.ganamd_prelu_bwd_bwd(ptr(ggx), ptr(gga), ptr(gy), ptr(x), ptr(a), C, L, ptr(g_gy), ptr(g_x),
                                        ptr(g_a), ptr(ws), stream()), "prelu_bwd_bwd")
+        if tgt is not None:
+            tgt.add_(g_a)          # one tiny add; the kernel has no accumulate form
+            g_a = None
         return g_gy, g_x, g_a
 
 
@@ -373,6 +434,7 @@ class BNAct(Function):
                                     ptr(ws), stream()), "bn_act_fwd")
         ctx.save_for_backward(x, gamma, beta, alpha, mean, invstd)
         ctx.has_alpha = alpha is not None
+        ctx.args = (gamma, beta, alpha)
         return y
 
     @staticmethod
@@ -382,12 +444,21 @@ class BNAct(Function):
         gy = _c(gy)
         C, L = _rows(x)
         gx = torch.empty_like(x)
-        gg = torch.empty_like(gamma)
-        gb = torch.empty_like(beta)
-        ga = torch.empty_like(alpha) if ctx.has_alpha else None
+        # parameter gradients straight into the flat buffer when all of them live there
+        tg = [flat_grad(a) if (a is not None and ctx.needs_input_grad[1 + i]) else None
+              for i, a in enumerate(ctx.args)]
+        direct = tg[0] is not None and tg[1] is not None and (not ctx.has_alpha or tg[2] is not None)
+        if direct:
+            gg, gb, ga = tg
+        else:
+            gg = torch.empty_like(gamma)
+            gb = torch.empty_like(beta)
+            ga = torch.empty_like(alpha) if ctx.has_alpha else None
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
         check(LIB.ganamd_bn_act_bwd(ptr(gy), ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(mean), ptr(invstd),
-                                    ptr(gx), ptr(gg), ptr(gb), ptr(ga), ptr(ws), stream()), "bn_act_bwd")
+                                    ptr(gx), ptr(gg), ptr(gb), ptr(ga), int(direct), ptr(ws), stream()), "bn_act_bwd")
+        if direct:
+            return gx, None, None, None, None, None, None, None
         return gx, gg, gb, ga, None, None, None, None
 
 
@@ -479,6 +550,7 @@ class ModConv(Function):
 
     @staticmethod
     def forward(ctx, x, s, d, w, geo, c):
+        ctx.w_arg = w
         x, s, d, w = _c(x), _c(s), _c(d), _c(w)
         y = _conv_fwd(geo, x, w, None, s, d, c)
         ctx.save_for_backward(x, s, d, w, y)
@@ -494,14 +566,20 @@ class ModConv(Function):
         gx = gs = gd = gw = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             gxs = _conv_dgrad(geo, gy, w, d, c)             # d/d(x*s)
-            if ctx.needs_input_grad[0]:
-                gx = gxs * s[:, :, None, None]
-            if ctx.needs_input_grad[1]:
-                gs = plane_dot(gxs, x)
+            # one pass: gx = gxs * s, gs = <gxs, x> per plane (ganamd_mix_bwd with M = 1)
+            gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+            gs = torch.empty_like(s) if ctx.needs_input_grad[1] else None
+            P, HW = _planes(x)
+            check(LIB.ganamd_mix_bwd(1, ptr(x), None, None, None, ptr(s), P, HW, ptr(gxs), ptr(gx), None, None, None,
+                                     ptr(gs), stream()), "mix_bwd")
         if ctx.needs_input_grad[2]:
             gd = plane_dot(gy, y) / d                       # y = d * conv  =>  dL/dd = sum gy*conv
         if ctx.needs_input_grad[3]:
-            gw = _conv_wgrad(geo, x, gy, s, d, c)
+            tgt = flat_grad(ctx.w_arg)
+            if tgt is not None:
+                _conv_wgrad(geo, x, gy, s, d, c, out=tgt, accumulate=True)
+            else:
+                gw = _conv_wgrad(geo, x, gy, s, d, c)
         return gx, gs, gd, gw, None, None
 
 
@@ -630,6 +708,7 @@ class AddPReLU(Function):
 
     @staticmethod
     def forward(ctx, a, b, alpha):
+        ctx.alpha_arg = alpha
         a, b = _c(a), _c(b)
         C, L = _rows(a)
         _need(alpha, C, "add_prelu alpha")
@@ -645,11 +724,12 @@ class AddPReLU(Function):
         z = a + b
         C, L = _rows(z)
         gz = torch.empty_like(z)
-        ga = torch.empty_like(alpha)
+        tgt = flat_grad(ctx.alpha_arg) if ctx.needs_input_grad[2] else None
+        ga = tgt if tgt is not None else torch.empty_like(alpha)
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), z.device)
-        check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(z), ptr(alpha), C, L, ptr(gz), ptr(ga), ptr(ws), stream()),
-              "prelu_bwd")
-        return gz, gz, ga
+        check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(z), ptr(alpha), C, L, ptr(gz), ptr(ga), int(tgt is not None),
+                                   ptr(ws), stream()), "prelu_bwd")
+        return gz, gz, (None if tgt is not None else ga)
 
 
 def add_prelu(a, b, alpha):

@@ -264,15 +264,13 @@ def _bn_fwd(x, C, L, gamma, beta, alpha, rm, rv):
     return y, mean, invstd
 
 
-def _bn_bwd(gy, x, C, L, gamma, beta, alpha, mean, invstd):
+def _bn_bwd(gy, x, C, L, gamma, beta, alpha, mean, invstd, gg, gb, ga):
+    """gx; the parameter gradients are ACCUMULATED into gg/gb/ga (flat-buffer regions)."""
     gx = torch.empty_like(x)
-    gg = torch.empty(C, device=x.device)
-    gb = torch.empty_like(gg)
-    ga = torch.empty_like(gg) if alpha is not None else None
     ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
     check(LIB.ganamd_bn_act_bwd(ptr(gy), ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(mean), ptr(invstd),
-                                ptr(gx), ptr(gg), ptr(gb), ptr(ga), ptr(ws), stream()), "bn_act_bwd")
-    return gx, gg, gb, ga
+                                ptr(gx), ptr(gg), ptr(gb), ptr(ga), 1, ptr(ws), stream()), "bn_act_bwd")
+    return gx
 
 
 class _BankFn(Function):
@@ -322,22 +320,18 @@ class _BankFn(Function):
             bank.pgrad(f"Wc{k}").view(gn, kk).addcmul_(bank.pdata(f"Wc{k}").view(gn, kk), gWsq[g0:g0 + gn, None],
                                                      value=2.0)
         # second BatchNorm (no activation)
-        gSp, gg2, gb2, _ = _bn_bwd(gS, Sp, bank.S_rows, B, bank.pdata("g2"), bank.pdata("be2"), None, m2, i2)
-        bank.pgrad("g2").add_(gg2)
-        bank.pgrad("be2").add_(gb2)
+        gSp = _bn_bwd(gS, Sp, bank.S_rows, B, bank.pdata("g2"), bank.pdata("be2"), None, m2, i2, bank.pgrad("g2"),
+                      bank.pgrad("be2"), None)
         # second linear (grouped)
-        bank.pgrad("b2").add_(gSp.sum(1))
+        ops.row_sum_acc(gSp, bank.pgrad("b2"))
         gY1 = torch.empty_like(Y1)
         grouped_gemm(bank.pdata("W2"), gSp, gY1, T["L2T"], a_trans=True)
         grouped_gemm(gSp, Y1, bank.pgrad("W2"), T["GW2"], b_trans=True)
         # first BatchNorm + PReLU
-        gH1, gg1, gb1, ga1 = _bn_bwd(gY1, H1, n * dl, B, bank.pdata("g1"), bank.pdata("be1"), bank.pdata("a1"), m1,
-                                     i1)
-        bank.pgrad("g1").add_(gg1)
-        bank.pgrad("be1").add_(gb1)
-        bank.pgrad("a1").add_(ga1)
+        gH1 = _bn_bwd(gY1, H1, n * dl, B, bank.pdata("g1"), bank.pdata("be1"), bank.pdata("a1"), m1, i1,
+                      bank.pgrad("g1"), bank.pgrad("be1"), bank.pgrad("a1"))
         # first linear (one stacked GEMM)
-        bank.pgrad("b1").add_(gH1.sum(1))
+        ops.row_sum_acc(gH1, bank.pgrad("b1"))
         geo1 = ops.linear_geo(B, dl, n * dl)
         ops._conv_wgrad(geo1, w, gH1, alpha=bank.c1, out=bank.pgrad("W1"), accumulate=True)
         gw = ops._conv_dgrad(geo1, gH1, bank.pdata("W1"), alpha=bank.c1).view(dl, B)

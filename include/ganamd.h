@@ -111,20 +111,22 @@ int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const f
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
                       float* save_mean, float* save_invstd, void* workspace, hipStream_t stream);
 
-/* Backward of ganamd_bn_act_fwd: writes gx [C][L], ggamma, gbeta, galpha ([C]; galpha may be
- * NULL when alpha is NULL). */
+/* Backward of ganamd_bn_act_fwd: writes gx [C][L]; ggamma, gbeta, galpha ([C]; galpha may be
+ * NULL when alpha is NULL) are overwritten, or accumulated into when accumulate = 1 (parameter
+ * gradients written straight into an optimizer's flat gradient buffer). */
 int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,
                       const float* alpha, const float* save_mean, const float* save_invstd, float* gx,
-                      float* ggamma, float* gbeta, float* galpha, void* workspace, hipStream_t stream);
+                      float* ggamma, float* gbeta, float* galpha, int accumulate, void* workspace,
+                      hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * PReLU (per-channel slope) with first and second derivatives (nn.PReLU; the critic's
  * gradient penalty differentiates through its backward: wgangp.py:47-50,69).
  * ------------------------------------------------------------------------------------- */
 int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y, hipStream_t stream);
-/* gx = gy * (x>0 ? 1 : alpha); galpha[c] = sum gy*x over x<=0 */
+/* gx = gy * (x>0 ? 1 : alpha); galpha[c] (=|+= with accumulate) sum gy*x over x<=0 */
 int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C, long L, float* gx, float* galpha,
-                     void* workspace, hipStream_t stream);
+                     int accumulate, void* workspace, hipStream_t stream);
 /* Backward of ganamd_prelu_bwd given ggx = dR/dgx and ggalpha = dR/dgalpha (may be NULL):
  *   ggy = ggx*(x>0?1:alpha) + ggalpha[c]*(x>0?0:x)
  *   gx  = ggalpha[c]*gy*(x>0?0:1)            (may be NULL)
@@ -151,8 +153,10 @@ int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int
 int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float scale, float* out,
                      hipStream_t stream);
 
-/* out[c] = sum_{l} a[c][l] * (b ? b[c][l] : 1) over rows of length L. */
-int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, void* workspace, hipStream_t stream);
+/* out[c] (=|+= with accumulate) sum_{l} a[c][l] * (b ? b[c][l] : 1) over rows of length L
+ * (with b = NULL and accumulate = 1: a conv bias gradient added into the flat gradient buffer). */
+int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, int accumulate, void* workspace,
+                   hipStream_t stream);
 
 /* out[i] = sum_{t<T} w[i*T + t]^2  (row sums of squares; the demodulation norm's sum over taps) */
 int ganamd_segment_sumsq(const float* w, long rows, int T, float* out, hipStream_t stream);

@@ -271,10 +271,13 @@ def test_resample_and_adjoint(ops, kind, n):
     assert rel(xa.grad, gx) < 1e-5
 
 
-def test_plane_mean(ops):
-    x = torch.randn(7, 4, 8, 8, dtype=torch.float64)
+@pytest.mark.parametrize("H", [8, 64])
+def test_plane_mean_and_dot(ops, H):
+    x = torch.randn(7, 4, H, H, dtype=torch.float64)
+    y = torch.randn(7, 4, H, H, dtype=torch.float64)
     xa = x.float().to(DEV)
     assert rel(ops.plane_mean(xa), x.mean(dim=(2, 3))) < 1e-6
+    assert rel(ops.plane_dot(xa, y.float().to(DEV)), (x * y).sum(dim=(2, 3))) < 1e-5
 
 
 def test_adamw_matches_torch():
@@ -383,7 +386,7 @@ def test_packed_weight_cache_tracks_updates(ops):
     assert rel(run(), y1) > 1e-3
 
 
-@pytest.mark.parametrize("M,H", [(2, 8), (2, 5), (3, 4), (1, 16)])
+@pytest.mark.parametrize("M,H", [(2, 8), (2, 5), (3, 4), (1, 16), (2, 32), (1, 64)])
 def test_mix_fwd_bwd(ops, M, H):
     g = torch.Generator().manual_seed(M * 10 + H)
     C, B = 6, 4
