@@ -8,5 +8,7 @@ from .generator_13_5 import Generator
 from .optim import FusedAdamW
 from .rng import DeviceRNG, ReplayRNG
 from .wgangp import Train
+from . import wganlazygpR2
+from . import generator_3_progan, discriminator_3_wgangp_progan
 
-__all__ = ["Generator", "Discriminator", "Train", "FusedAdamW", "DeviceRNG", "ReplayRNG"]
+__all__ = ["Generator", "Discriminator", "Train", "FusedAdamW", "DeviceRNG", "ReplayRNG", "wganlazygpR2", "generator_3_progan", "discriminator_3_wgangp_progan"]

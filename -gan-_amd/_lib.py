@@ -64,6 +64,9 @@ _SIGS = {
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),
     "ganamd_adamw": (c_int, [vp, vp, vp, vp, c_long, vp, c_float, c_float, c_float, c_float, c_float, vp]),
     "ganamd_grouped_gemm": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp]),
+    "ganamd_image_batch_workspace": (c_size_t, [c_int, c_int, c_int]),
+    "ganamd_image_batch": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, c_int, c_int, vp, vp, c_int, c_int, vp, vp,
+                                   vp, vp, vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -1,0 +1,78 @@
+"""Checkpoint save / resume of the trainers (reference: train/trainunits.py:58-130).
+
+Kept from the reference: the file naming (``checkpoint/<G name> <D name> <method> epoch_<E>
+i_<I>_ckpt.pth``), the fields ``generator_name``, ``discriminator_name``, ``method``, ``epoch``,
+``i`` with the same epoch/i carry arithmetic, and ``load_*_ckpt(name)`` reading
+``checkpoint/<name>.pth`` and doing nothing when it is absent.
+
+Changed: the reference pickles whole modules and, on load, rebinds
+``self.generator`` while the optimizers keep the old parameters (they silently stop training
+the loaded network).  Here ``generator`` / ``discriminator`` are ``state_dict()``s keyed by the
+reference's own parameter/buffer names (drop-in and reference modules load each other's), they
+are loaded IN PLACE (the flat-buffer views and the optimizers stay bound), and the optimizer
+moments and step counters are saved too.  Everything is tensors/str/int, so
+``torch.load(..., weights_only=True)`` reads it.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def _cpu_state(module):
+    return {k: v.detach().to("cpu", copy=True) for k, v in module.state_dict().items()}
+
+
+def ckpt_path(root, g_name, d_name, method, epoch, i):
+    return os.path.join(root, f"{g_name} {d_name} {method} epoch_{epoch} i_{i}_ckpt.pth")
+
+
+class CheckpointMixin:
+    """Mixed into the trainers; needs generator(_name), discriminator(_name), optimizer_G/D,
+    and the epoch bookkeeping ``epoch``, ``i``, ``epoch_len``."""
+
+    ckpt_root = "checkpoint"
+
+    def _ckpt_counters(self, epoch, i):
+        e = epoch + self.epoch + (i + self.i) // self.epoch_len
+        return e, (i + self.i) % self.epoch_len
+
+    def save_ckpt(self, train_name, epoch, i):
+        """trainunits.py:58-77 (state_dicts + optimizer state instead of pickled modules)."""
+        e, ii = self._ckpt_counters(epoch, i)
+        state = {"generator": _cpu_state(self.generator), "generator_name": self.generator_name,
+                 "discriminator": _cpu_state(self.discriminator), "discriminator_name": self.discriminator_name,
+                 "method": train_name, "epoch": e, "i": ii,
+                 "optimizer_G": self.optimizer_G.state_dict(), "optimizer_D": self.optimizer_D.state_dict()}
+        os.makedirs(self.ckpt_root, exist_ok=True)
+        path = ckpt_path(self.ckpt_root, self.generator_name, self.discriminator_name, train_name, e, ii)
+        torch.save(state, path)
+        return path
+
+    def _load(self, name):
+        path = os.path.join(self.ckpt_root, name + ".pth")
+        if not os.path.isfile(path):
+            return None
+        return torch.load(path, map_location="cpu", weights_only=True)
+
+    def load_generator_ckpt(self, name):
+        """trainunits.py:93-111: also restores epoch / i; loads in place."""
+        ck = self._load(name)
+        if ck is None:
+            return False
+        self.generator.load_state_dict(ck["generator"])
+        if "optimizer_G" in ck:
+            self.optimizer_G.load_state_dict(ck["optimizer_G"])
+        self.epoch, self.i = int(ck["epoch"]), int(ck["i"])
+        return True
+
+    def load_discriminator_ckpt(self, name):
+        """trainunits.py:113-128."""
+        ck = self._load(name)
+        if ck is None:
+            return False
+        self.discriminator.load_state_dict(ck["discriminator"])
+        if "optimizer_D" in ck:
+            self.optimizer_D.load_state_dict(ck["optimizer_D"])
+        return True

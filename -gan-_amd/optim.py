@@ -75,6 +75,20 @@ class FusedAdamW:
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 
+    def state_dict(self):
+        """Moments over the trainable flat range + the step counter (checkpoint.py)."""
+        return {"exp_avg": self.exp_avg.detach().cpu(), "exp_avg_sq": self.exp_avg_sq.detach().cpu(),
+                "step": self.step_count.detach().cpu(), "n_train": self.flat.n_train,
+                "lr": self.lr, "betas": list(self.betas), "eps": self.eps, "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd):
+        if int(sd["n_train"]) != self.flat.n_train:
+            raise ValueError(f"optimizer state for {sd['n_train']} parameters, this model trains {self.flat.n_train}")
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.step_count.copy_(sd["step"])
+        self.flat.epoch += 1      # parameters may have been reloaded: packed conv weights are stale
+
     @torch.no_grad()
     def step(self):
         f = self.flat

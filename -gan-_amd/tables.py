@@ -72,6 +72,34 @@ def adaptive_pool_1d(n, out):
     return m
 
 
+def _aa_cubic(x, a=-0.5):
+    """Keys cubic with a = -0.5: the filter of torch's antialiased bicubic (as PIL's)."""
+    x = abs(x)
+    if x < 1.0:
+        return ((a + 2) * x - (a + 3)) * x * x + 1
+    if x < 2.0:
+        return ((a * x - 5 * a) * x + 8 * a) * x - 4 * a
+    return 0.0
+
+
+def bicubic_aa_1d(n_in, n_out):
+    """F.interpolate(mode='bicubic', antialias=True, align_corners=False) along one axis, the
+    Resize of torchvision's tensor path (units/dataloader.py:11): for scale = n_in/n_out >= 1 the
+    cubic is stretched by the scale (support 2*scale) and every row renormalised to sum 1."""
+    scale = n_in / n_out
+    support = 2.0 * scale if scale >= 1.0 else 2.0
+    inv = 1.0 / scale if scale >= 1.0 else 1.0
+    m = np.zeros((n_out, n_in))
+    for o in range(n_out):
+        center = scale * (o + 0.5)
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), n_in)
+        w = np.asarray([_aa_cubic((j + xmin - center + 0.5) * inv) for j in range(xmax - xmin)])
+        tot = w.sum()
+        m[o, xmin:xmax] = w / tot if tot != 0 else w
+    return m
+
+
 def operator_1d(kind: str, n: int) -> np.ndarray:
     if kind == "smooth":
         return smooth_1d(n)

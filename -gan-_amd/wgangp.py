@@ -23,6 +23,7 @@ import contextlib
 
 import torch
 
+from .checkpoint import CheckpointMixin
 from .optim import FusedAdamW
 from .rng import DeviceRNG
 
@@ -39,7 +40,7 @@ def _frozen(module):
             p.requires_grad_(True)
 
 
-class Train:
+class Train(CheckpointMixin):
     def __init__(self, dataloader, device, num_epochs, nz, generator, generator_name, discriminator,
                  discriminator_name, rng=None):
         self.dataloader = dataloader
@@ -49,11 +50,23 @@ class Train:
         self.generator, self.generator_name = generator, generator_name
         self.discriminator, self.discriminator_name = discriminator, discriminator_name
         self.rng = rng if rng is not None else DeviceRNG(self.device)
-        self.optimizer_G = FusedAdamW(generator, lr=0.0001, betas=(0.5, 0.999))
-        self.optimizer_D = FusedAdamW(discriminator, lr=0.0004, betas=(0.5, 0.999))
+        self.optimizer_G, self.optimizer_D = self.make_optimizers()
+        # epoch bookkeeping of train/trainunits.py:25-28 (checkpoint names and resume)
+        self.epoch, self.i = 0, 0
+        try:
+            self.epoch_len = max(1, len(dataloader))
+        except TypeError:
+            self.epoch_len = 1
+
+    def make_optimizers(self):
+        """train/wgangp.py:17-18: AdamW (weight_decay 0.01), G lr 1e-4, D lr 4e-4, betas (0.5, 0.999)."""
+        return (FusedAdamW(self.generator, lr=0.0001, betas=(0.5, 0.999)),
+                FusedAdamW(self.discriminator, lr=0.0004, betas=(0.5, 0.999)))
 
     def _generate(self, z):
-        self.generator.noise_hub.source = self.rng.noise
+        hub = getattr(self.generator, "noise_hub", None)      # G13_5's in-forward noise (progan has none)
+        if hub is not None:
+            hub.source = self.rng.noise
         return self.generator(z)
 
     def generator_trainstep(self, b_size):
@@ -119,11 +132,18 @@ class Train:
         gp.backward()
         return real_loss, fake_loss, gp
 
-    def train(self):
-        """Epoch loop of train/wgangp.py:73-95 without the display / checkpoint side work."""
-        for _epoch in range(self.num_epochs):
+    def train(self, checkpoints=True):
+        """Epoch loop of train/wgangp.py:73-95: resume from ``checkpoint/.pth`` if present, one
+        critic step + one generator step per batch, a checkpoint after every epoch (display and
+        image-grid side work left out)."""
+        if checkpoints:
+            self.load_generator_ckpt("")
+            self.load_discriminator_ckpt("")
+        for epoch in range(self.num_epochs):
             for images, _ in self.dataloader:
                 images = images.to(self.device)
                 b = images.shape[0]
                 self.discriminator_trainstep(images, b)
                 self.generator_trainstep(b)
+            if checkpoints:
+                self.save_ckpt("WGANGP", epoch + 1, 0)

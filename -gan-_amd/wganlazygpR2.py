@@ -1,0 +1,86 @@
+"""Drop-in lazy-GP + R1/R2 trainer (reference: train/wganlazygpR2.py ``Train``, optimizers of
+train/trainunits.py:18-19).
+
+Step semantics kept (wganlazygpR2.py:17-77):
+  * generator step: -mean D(G(z)), Adam lr 1e-4, betas (0.5, 0.99), no weight decay;
+  * critic step ``idx``: no-grad G forward, real loss -mean D(x), fake loss mean D(G(z)); when
+    ``idx % 5 == 0`` additionally R1 = 5 * mean_i |grad_x D(x_i)|^2 on the real batch, R2 the same
+    on the fake batch, and GP = 10 * 5 * mean((|grad D(x_hat)| - 1)^2) on eps-interpolated samples
+    (eps ~ U[0,1) per sample, drawn after z and the generator noise); Adam lr 4e-4, betas
+    (0.0, 0.99).  Returns (real_loss, fake_loss, gp, r2_reg_r, r2_reg_f) with zeros [1] for the
+    terms a step does not compute.
+
+Differences that do not change what is trained (same kind as wgangp.py's):
+  * The reference runs up to five backward calls per critic step; their gradients accumulate,
+    so one backward of the summed objective gives the same parameter gradients.
+  * The critic sees the real, fake (and interpolated) batches as ONE pass of 2B (3B) samples with
+    per-segment MiniBatchStdDev (Discriminator.forward ``segments``): every other layer is
+    per-sample, so the outputs, the per-sample input gradients that R1/R2/GP square, and the
+    summed weight gradients are those of the reference's separate passes.
+  * The input gradients the reference leaves in ``images.grad`` / ``gen_imgs.grad`` are never
+    read (dead work, skipped); as in wgangp.py the critic's weight gradient in the generator step
+    is not computed.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import wgangp
+from .optim import FusedAdamW
+
+LAZY_INTERVAL = 5      # wganlazygpR2.py:56,65,71: regularisers every 5th critic step
+REG_WEIGHT = 5         # R1 / R2 weight (:58, :67) and the lazy GP multiplier (:72)
+GP_LAMBDA = 10         # :72
+
+
+class Train(wgangp.Train):
+    def make_optimizers(self):
+        """trainunits.py:18-19: torch.optim.Adam (weight_decay 0)."""
+        return (FusedAdamW(self.generator, lr=0.0001, betas=(0.5, 0.99), weight_decay=0.0),
+                FusedAdamW(self.discriminator, lr=0.0004, betas=(0.0, 0.99), weight_decay=0.0))
+
+    def discriminator_trainstep(self, images, b_size, idx):
+        """wganlazygpR2.py:48-77."""
+        out = self.discriminator_backward(images, b_size, idx)
+        self.optimizer_D.step()
+        return out
+
+    def discriminator_backward(self, images, b_size, idx):
+        self.optimizer_D.zero_grad()
+        z = self.rng.randn((b_size, self.nz, 1, 1))
+        with torch.no_grad():
+            gen_imgs = self._generate(z)
+        images = images.detach()
+        if idx % LAZY_INTERVAL != 0:
+            pred = self.discriminator(torch.cat([images, gen_imgs]), segments=2)
+            real_loss = -torch.mean(pred[:b_size])
+            fake_loss = torch.mean(pred[b_size:])
+            (real_loss + fake_loss).backward()
+            zero = torch.zeros(1, device=images.device)
+            return real_loss, fake_loss, zero, zero.clone(), zero.clone()
+        eps = self.rng.rand((b_size,)).view(b_size, 1, 1, 1)
+        x_interp = (1 - eps) * images + eps * gen_imgs
+        x = torch.cat([images, gen_imgs, x_interp]).detach().requires_grad_()
+        pred = self.discriminator(x, segments=3)
+        grad = torch.autograd.grad(pred.sum(), x, create_graph=True, retain_graph=True, only_inputs=True)[0]
+        g2 = grad.pow(2).view(3 * b_size, -1).sum(1)
+        real_loss = -torch.mean(pred[:b_size])
+        fake_loss = torch.mean(pred[b_size:2 * b_size])
+        r2_reg_r = REG_WEIGHT * g2[:b_size].mean()
+        r2_reg_f = REG_WEIGHT * g2[b_size:2 * b_size].mean()
+        gp = GP_LAMBDA * (g2[2 * b_size:].sqrt() - 1.0).pow(2).mean() * REG_WEIGHT
+        (real_loss + fake_loss + r2_reg_r + r2_reg_f + gp).backward()
+        return real_loss, fake_loss, gp, r2_reg_r, r2_reg_f
+
+    def train(self, checkpoints=True):
+        """Epoch loop of wganlazygpR2.py:79-121 (resume from ``checkpoint/.pth`` if present; the
+        reference saves no checkpoint here, :121 is commented out; display side work left out)."""
+        if checkpoints:
+            self.load_generator_ckpt("")
+            self.load_discriminator_ckpt("")
+        for _epoch in range(self.num_epochs):
+            for i, (images, _) in enumerate(self.dataloader):
+                images = images.to(self.device)
+                b = images.shape[0]
+                self.discriminator_trainstep(images, b, i)
+                self.generator_trainstep(b)

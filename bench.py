@@ -44,7 +44,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="images per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
+    ap.add_argument("--config", choices=["wgangp", "lazy", "progan"], default="wgangp",
+                    help="wgangp = the headline (configs 2/3); lazy = config 4 (fp32); progan = config 5")
     ap.add_argument("--mode", choices=["eager", "graph"], default="graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -138,47 +140,75 @@ def roofline_probe(dev, reps=20):
     return out
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist(args.gpus, args.backend)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    import gan_amd
-    from gan_amd import ops
-    from gan_amd.dist import allreduce_mean_, attach_grad_sync
+CONFIGS = {
+    # name: (metric, default per-GPU batch, description)
+    "wgangp": (METRIC, 64, "G13_5+D9_4 WGAN-GP iteration (5 critic steps with GP + 1 generator step), 64x64x3"),
+    "lazy": ("images/sec per lazy-GP+R1/R2 period (G13_5+D9_4, 64x64, wganlazygpR2, 5 batches)", 128,
+             "G13_5+D9_4 train/wganlazygpR2.py: 5 batches = 5 x (critic step + generator step), R1/R2/GP on the "
+             "first, Adam; config 4 of BASELINE.json (fp32 here)"),
+    "progan": ("images/sec per WGAN-GP iter (generator_3_progan ngf=256 + discriminator_3_wgangp_progan ndf=64, "
+               "64x64, n_critic=5)", 64,
+               "progan pair under train/wgangp.py, fixed 64x64 nets (the reference has no progressive schedule); "
+               "config 5 of BASELINE.json at 64 images per GPU"),
+}
 
+
+def build(args, dev, rank):
+    """Models, trainer, and the iteration as a list of optimizer phases:
+    (graph key, backward callable, optimizer, images it consumes)."""
+    import gan_amd
     torch.manual_seed(1234)                         # identical initial weights on every rank
-    G = gan_amd.Generator(256).to(dev)
-    G.use_bank = not args.no_bank
-    D = gan_amd.Discriminator().to(dev)
+    if args.config == "progan":
+        G = gan_amd.generator_3_progan.Generator(1, 256, 256, 3).to(dev)
+        D = gan_amd.discriminator_3_wgangp_progan.Discriminator(1, 64, 3).to(dev)
+    else:
+        G = gan_amd.Generator(256).to(dev)
+        G.use_bank = not args.no_bank
+        D = gan_amd.Discriminator().to(dev)
     torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
-    tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev))
-    if world > 1 and args.mode == "eager":
-        attach_grad_sync(tr.optimizer_G)
-        attach_grad_sync(tr.optimizer_D)
+    Tr = gan_amd.wganlazygpR2.Train if args.config == "lazy" else gan_amd.Train
+    tr = Tr([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev))
     B = args.batch
 
-    def iteration():
-        for _ in range(N_CRITIC):
-            images = torch.randn(B, 3, 64, 64, device=dev)
-            tr.discriminator_trainstep(images, B)
-        tr.generator_trainstep(B)
+    def real():
+        return torch.randn(B, 3, 64, 64, device=dev)
+
+    gen = ("gen", lambda: tr.generator_backward(B), tr.optimizer_G, 0)
+    if args.config == "lazy":
+        phases = []
+        for idx in range(5):     # one lazy period: the regularised critic step, then 4 plain ones
+            key = "critic_reg" if idx == 0 else "critic"
+            phases += [(key, (lambda i=idx: tr.discriminator_backward(real(), B, i)), tr.optimizer_D, B), gen]
+    else:
+        crit = ("critic", lambda: tr.discriminator_backward(real(), B), tr.optimizer_D, B)
+        phases = [crit] * N_CRITIC + [gen]
+    return G, D, tr, phases
+
+
+def main():
+    args = parse()
+    if args.batch is None:
+        args.batch = CONFIGS[args.config][1]
+    world, rank, local = setup_dist(args.gpus, args.backend)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    from gan_amd import ops
+    from gan_amd.dist import allreduce_mean_
+
+    G, D, tr, phases = build(args, dev, rank)
+    B = args.batch
+    headline = args.config == "wgangp"
+    # images per iteration per GPU: the generator-step batches (wgangp: 1 per n_critic critic steps)
+    imgs_per_iter = B * sum(1 for k, *_ in phases if k == "gen")
 
     def sync(opt):
         if world > 1:
             allreduce_mean_(opt.flat.grad)
 
-    def iteration_split():
-        # the same iteration with the gradient all-reduce outside the optimizer (graph mode)
-        for _ in range(N_CRITIC):
-            tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B)
-            sync(tr.optimizer_D)
-            tr.optimizer_D.step()
-        tr.generator_backward(B)
-        sync(tr.optimizer_G)
-        tr.optimizer_G.step()
-
-    if args.mode == "graph" and world > 1:
-        iteration = iteration_split
+    def iteration():
+        for _key, bwd, opt, _ in phases:
+            bwd()
+            sync(opt)
+            opt.step()
 
     # warm-up (eager); the first one also counts the conv FLOPs this build issues
     ops.FlopCounter.enabled = True
@@ -190,12 +220,12 @@ def main():
     torch.cuda.synchronize()
 
     step = iteration
+    graphs = {}
     if args.mode == "graph":
-        # one HIP graph per critic step and one per generator step (the synthetic real batch,
-        # z, noise and eps are drawn inside the graphs; torch advances the Philox offsets on
-        # every replay), replayed 5 + 1 times per iteration
-        # With N > 1 ranks the RCCL all-reduce of the flat gradient runs eagerly between a
-        # forward/backward graph and an optimizer graph (collectives are kept out of capture).
+        # one HIP graph per distinct phase (synthetic real batch, z, noise and eps are drawn
+        # inside; torch advances the Philox offsets on every replay).  N = 1: backward + optimizer
+        # in one graph.  N > 1: the RCCL all-reduce of the flat gradient runs eagerly between a
+        # backward graph and an optimizer graph (collectives are kept out of capture).
         def capture(fn):
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -207,30 +237,22 @@ def main():
                 fn()
             return g
 
-        if world == 1:
-            gd = capture(lambda: tr.discriminator_trainstep(torch.randn(B, 3, 64, 64, device=dev), B))
-            gg = capture(lambda: tr.generator_trainstep(B))
-            torch.cuda.synchronize()
+        for key, bwd, opt, _ in phases:
+            if key in graphs:
+                continue
+            if world == 1:
+                graphs[key] = (capture(lambda b=bwd, o=opt: (b(), o.step())), None, opt)
+            else:
+                graphs[key] = (capture(bwd), capture(opt.step), opt)
+        torch.cuda.synchronize()
 
-            def step():
-                for _ in range(N_CRITIC):
-                    gd.replay()
-                gg.replay()
-        else:
-            gd = capture(lambda: tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B))
-            gdo = capture(tr.optimizer_D.step)
-            gg = capture(lambda: tr.generator_backward(B))
-            ggo = capture(tr.optimizer_G.step)
-            torch.cuda.synchronize()
-
-            def step():
-                for _ in range(N_CRITIC):
-                    gd.replay()
-                    allreduce_mean_(tr.optimizer_D.flat.grad)
-                    gdo.replay()
-                gg.replay()
-                allreduce_mean_(tr.optimizer_G.flat.grad)
-                ggo.replay()
+        def step():
+            for key, *_ in phases:
+                gb, go, opt = graphs[key]
+                gb.replay()
+                if go is not None:
+                    allreduce_mean_(opt.flat.grad)
+                    go.replay()
 
     if world > 1:
         dist.barrier()
@@ -252,53 +274,27 @@ def main():
     secs = float(t)
 
     if rank == 0 and args.mode == "graph" and world == 1 and not args.no_extras:
-        # breakdown (outside the timed region): one critic-step graph, one generator-step graph
+        # breakdown (outside the timed region): one replay per phase graph
         parts = {}
-        for name, g in (("critic_step", gd), ("generator_step", gg)):
+        for key, (g, _, _) in graphs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             g.replay()
             e1.record()
             torch.cuda.synchronize()
-            parts[name] = round(e0.elapsed_time(e1), 1)
-        # eager pieces of the critic step (indicative; eager adds launch gaps)
-        def timed(fn, n=2):
-            fn()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(n):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            return round(e0.elapsed_time(e1) / n, 1)
-
-        z = torch.randn(B, 256, 1, 1, device=dev)
-        x2 = torch.randn(2 * B, 3, 64, 64, device=dev)
-
-        def g_fwd():
-            with torch.no_grad():
-                G(z)
-
-        def d_fwd_bwd():
-            D(x2, segments=2).sum().backward()
-
-        def gp():
-            (10 * tr.gradient_penalty(x2[:B], x2[B:], B)).backward()
-
-        parts.update(eager_g_forward=timed(g_fwd), eager_d_fwd_bwd_2B=timed(d_fwd_bwd), eager_gp=timed(gp))
-        print(f"[bench] ms per graph / piece: {parts}", file=sys.stderr, flush=True)
+            parts[key] = round(e0.elapsed_time(e1), 1)
+        print(f"[bench] ms per phase graph: {parts}", file=sys.stderr, flush=True)
     probe = None
-    if rank == 0 and world == 1 and not args.no_extras:
+    if rank == 0 and world == 1 and headline and not args.no_extras:
         probe = roofline_probe(dev)
     if rank == 0:
         print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
               f"issued GEMM launches/iter {ops.FlopCounter.launches}", file=sys.stderr, flush=True)
-        n_img = B * world * args.steps
+        n_img = imgs_per_iter * world * args.steps
         t_iter = secs / args.steps
-        achieved = ALGO_GFLOP_PER_IMAGE * 1e9 * B / t_iter / 1e12      # per GPU
+        metric, _, desc = CONFIGS[args.config]
         out = {
-            "metric": METRIC,
+            "metric": metric,
             "value": n_img / secs,
             "unit": "images/sec",
             "n_gpus": world,
@@ -310,17 +306,24 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic N(0,1) real batches drawn on device each critic step; random reference-init weights",
-            "config": {"workload": "G13_5+D9_4 WGAN-GP iteration (5 critic steps with GP + 1 generator step), "
-                                   "64x64x3", "global_batch": B * world, "per_gpu_batch": B, "n_critic": N_CRITIC,
+            "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
                        "parallelism": f"dp{world}", "mode": args.mode},
-            "roofline": dict(probe or {}, **{
+        }
+        if headline:
+            out["config"]["n_critic"] = N_CRITIC
+            achieved = ALGO_GFLOP_PER_IMAGE * 1e9 * B / t_iter / 1e12      # per GPU
+            out["roofline"] = dict(probe or {}, **{
                 # whole iteration: algorithmic FLOPs / iteration time, per GPU
                 "iteration_tflops": achieved, "iteration_frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                 "algorithmic_gflop_per_iter": ALGO_GFLOP_PER_IMAGE * B,
-                "issued_gemm_gflop_per_iter": issued_flops / 1e9}),
-            "wall_s": wall,
-        }
-        if world == 1 and not args.no_cpu_baseline:
+                "issued_gemm_gflop_per_iter": issued_flops / 1e9})
+        else:
+            out["roofline"] = {"bound": "mfma", "issued_gemm_gflop_per_iter": issued_flops / 1e9,
+                               "achieved": issued_flops / t_iter / 1e12, "peak": FP32_MFMA_PEAK_TFLOPS,
+                               "unit": "TFLOP/s", "frac": issued_flops / t_iter / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                               "note": "issued conv-GEMM FLOPs of this build per iteration / iteration time"}
+        out["wall_s"] = wall
+        if world == 1 and headline and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -210,6 +210,19 @@ int ganamd_add_prelu(const float* a, const float* b, const float* alpha, int C, 
 int ganamd_scale_add(const float* x, const float* s, const float* r, long planes, long HW, float* y,
                      hipStream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Real-data input pipeline (units/dataloader.py:5-14): a batch of B
+ * decoded images u8 [B][H][W][3] (one size) -> f32 NCHW [B][3][OH][OW]:
+ *   ToTensor (/255) -> RandomHorizontalFlip (flip[b] != 0 mirrors image b; flip may be NULL)
+ *   -> Resize((OH, OW), BICUBIC, antialias) as separable ELL tap tables (ix/wx: OW x KX over
+ *   the W axis, iy/wy: OH x KY over the H axis) -> Normalize(mean[3], std[3]).
+ * workspace: ganamd_image_batch_workspace(B, H, OW) bytes (the row-pass intermediate).
+ * ------------------------------------------------------------------------------------- */
+size_t ganamd_image_batch_workspace(int B, int H, int OW);
+int ganamd_image_batch(const uint8_t* src, int B, int H, int W, const uint8_t* flip, const int32_t* ix,
+                       const float* wx, int KX, int OW, const int32_t* iy, const float* wy, int KY, int OH,
+                       const float* mean, const float* stdv, float* y, float* workspace, hipStream_t stream);
+
 /* Library identification (for load checks). */
 const char* ganamd_version(void);
 

@@ -427,6 +427,68 @@ def discriminator(P, x):
 
 
 # ----------------------------------------------------------------------------------------------
+# progan pair (generators/generator_3_progan.py, discriminators/discriminator_3_wgangp_progan.py)
+# ----------------------------------------------------------------------------------------------
+
+def progan_stages(ngf):
+    """(cin, cout, stride, pad) of the five ConvT k4 stages (generator_3_progan.py:43-50)."""
+    return [(None, ngf * 8, 1, 0), (ngf * 8, ngf * 4, 2, 1), (ngf * 4, ngf * 2, 2, 1),
+            (ngf * 2, ngf, 2, 1), (ngf, 3, 2, 1)]
+
+
+def progan_generator(P, z, randn=None, ngf=256):
+    """Generator.forward (generator_3_progan.py:33-54): [ConvT k4, BN2d, PReLU(1)] x 5, Tanh."""
+    x = z
+    for i, (cin, cout, s, p) in enumerate(progan_stages(ngf)):
+        cin = x.shape[1]
+        w = P(f"main.{i}.0.weight", (cin, cout, 4, 4), "convt")
+        b = P(f"main.{i}.0.bias", (cout,), "zeros")
+        x = F.conv_transpose2d(x, w, b, stride=s, padding=p)
+        x = bn(P, f"main.{i}.1", x, cout)
+        x = F.prelu(x, P(f"main.{i}.2.weight", (1,), "prelu"))
+    return torch.tanh(x)
+
+
+def progan_stddev(x):
+    """StandardDeviation (discriminator_3_wgangp_progan.py:7-16): batch std, eps 10e-8."""
+    b, _, h, w = x.shape
+    o = x - x.mean(dim=0, keepdim=True)
+    o = torch.sqrt(o.pow(2.0).mean(dim=0, keepdim=False) + 10e-8).mean().view(1, 1, 1, 1)
+    return torch.cat([x, o.repeat(b, 1, h, w)], 1)
+
+
+def progan_d_layers(ndf, nc=3):
+    """(cin, cout, k, stride, pad) of the EqualizedConv2d stack (discriminator_3_wgangp_progan.py:35-66);
+    None marks StandardDeviation."""
+    return [(nc, ndf, 1, 1, 0), (ndf, ndf, 3, 1, 1), (ndf, ndf, 3, 2, 1), (ndf, 2 * ndf, 3, 1, 1),
+            (2 * ndf, 2 * ndf, 3, 2, 1), (2 * ndf, 4 * ndf, 3, 1, 1), (4 * ndf, 4 * ndf, 3, 2, 1),
+            (4 * ndf, 8 * ndf, 3, 1, 1), (8 * ndf, 8 * ndf, 3, 2, 1), None, (8 * ndf + 1, 8 * ndf, 3, 1, 1),
+            (8 * ndf, 8 * ndf, 4, 1, 0), (8 * ndf, 1, 1, 1, 0)]
+
+
+def progan_discriminator(P, x, ndf=64):
+    """Discriminator.forward (discriminator_3_wgangp_progan.py:31-70): zero-padded
+    EqualizedConv2d (input scaled by sqrt(2)/sqrt(k*k*cin), :22,28-29), single-slope PReLU."""
+    idx = 0
+    layers = progan_d_layers(ndf)
+    for j, l in enumerate(layers):
+        if l is None:
+            x = progan_stddev(x)
+            idx += 1
+            continue
+        cin, cout, k, s, p = l
+        w = P(f"main.{idx}.conv.weight", (cout, cin, k, k))
+        b = P(f"main.{idx}.bias", (cout,))
+        scale = math.sqrt(2) / math.sqrt(k * k * cin)
+        x = F.conv2d(x * scale, w, None, stride=s, padding=p) + b.view(1, cout, 1, 1)
+        idx += 1
+        if j < len(layers) - 1:
+            x = F.prelu(x, P(f"main.{idx}.weight", (1,), "prelu"))
+            idx += 1
+    return x.view(x.shape[0], -1)
+
+
+# ----------------------------------------------------------------------------------------------
 # WGAN-GP steps (train/wgangp.py)
 # ----------------------------------------------------------------------------------------------
 
@@ -437,8 +499,10 @@ class WGANGP:
     in-forward noise, ``draw.rand(shape)`` for eps.
     """
 
-    def __init__(self, GP: Params, DP: Params, nz=256):
+    def __init__(self, GP: Params, DP: Params, nz=256, gen=None, disc=None):
         self.GP, self.DP, self.nz = GP, DP, nz
+        self.gen = gen or generator          # (P, z, randn) -> images
+        self.disc = disc or discriminator    # (P, x) -> [B, 1]
         # torch.optim.AdamW defaults (weight_decay 0.01, eps 1e-8) as wgangp.py:17-18
         self.g_order = list(GP.t.keys())
         self.d_order = list(DP.t.keys())
@@ -449,8 +513,8 @@ class WGANGP:
         """wgangp.py:20-27."""
         self.opt_G.zero_grad()
         z = draw.randn((b, self.nz, 1, 1))
-        gen = generator(self.GP, z, draw.randn)
-        g_loss = -torch.mean(discriminator(self.DP, gen))
+        gen = self.gen(self.GP, z, draw.randn)
+        g_loss = -torch.mean(self.disc(self.DP, gen))
         g_loss.backward()
         self.opt_G.step()
         return gen, g_loss
@@ -459,7 +523,7 @@ class WGANGP:
         """wgangp.py:34-54."""
         eps = draw.rand((b,)).view(b, 1, 1, 1)
         xi = ((1 - eps) * x_real + eps * x_fake).detach().requires_grad_()
-        d_out = discriminator(self.DP, xi)
+        d_out = self.disc(self.DP, xi)
         g = torch.autograd.grad(d_out.sum(), xi, create_graph=True, retain_graph=True, only_inputs=True)[0]
         g2 = g.pow(2).view(b, -1).sum(1)
         return (g2.sqrt() - center).pow(2).mean()
@@ -469,16 +533,63 @@ class WGANGP:
         self.opt_D.zero_grad()
         z = draw.randn((b, self.nz, 1, 1))
         with torch.no_grad():
-            gen = generator(self.GP, z, draw.randn)
+            gen = self.gen(self.GP, z, draw.randn)
         gen.requires_grad_()
-        real_loss = -torch.mean(discriminator(self.DP, images))
+        real_loss = -torch.mean(self.disc(self.DP, images))
         real_loss.backward()
-        fake_loss = torch.mean(discriminator(self.DP, gen))
+        fake_loss = torch.mean(self.disc(self.DP, gen))
         fake_loss.backward()
         gp = 10 * self.gradient_penalty(images, gen, b, draw)
         gp.backward()
         self.opt_D.step()
         return real_loss, fake_loss, gp
+
+
+class WGANLazyR2(WGANGP):
+    """The oracle counterpart of ``train/wganlazygpR2.py:Train`` with the optimizers of
+    ``train/trainunits.py:18-19`` (Adam, G lr 1e-4 betas (0.5, 0.99), D lr 4e-4 betas (0.0, 0.99)).
+    Follows the reference's call sequence literally: separate real / fake passes, one backward per
+    term (gradients accumulate)."""
+
+    def __init__(self, GP: Params, DP: Params, nz=256, gen=None, disc=None):
+        super().__init__(GP, DP, nz, gen, disc)
+        self.opt_G = torch.optim.Adam([GP.t[k] for k in self.g_order], lr=1e-4, betas=(0.5, 0.99))
+        self.opt_D = torch.optim.Adam([DP.t[k] for k in self.d_order], lr=4e-4, betas=(0.0, 0.99))
+
+    def compute_grad2(self, d_out, x_in):
+        """wganlazygpR2.py:37-46."""
+        g = torch.autograd.grad(d_out.sum(), x_in, create_graph=True, retain_graph=True, only_inputs=True)[0]
+        return g.pow(2).view(x_in.shape[0], -1).sum(1)
+
+    def discriminator_trainstep(self, images, b, idx, draw):
+        """wganlazygpR2.py:48-77."""
+        self.opt_D.zero_grad()
+        z = draw.randn((b, self.nz, 1, 1))
+        with torch.no_grad():
+            gen = self.gen(self.GP, z, draw.randn)
+        gen.requires_grad_()
+        images = images.detach().requires_grad_()
+        reg = idx % 5 == 0
+        pred_r = self.disc(self.DP, images)
+        real_loss = -torch.mean(pred_r)
+        r1 = torch.zeros(1)
+        real_loss.backward(retain_graph=reg)
+        if reg:
+            r1 = 5 * self.compute_grad2(pred_r, images).mean()
+            r1.backward()
+        pred_f = self.disc(self.DP, gen)
+        fake_loss = torch.mean(pred_f)
+        r2 = torch.zeros(1)
+        fake_loss.backward(retain_graph=reg)
+        if reg:
+            r2 = 5 * self.compute_grad2(pred_f, gen).mean()
+            r2.backward()
+        gp = torch.zeros(1)
+        if reg:
+            gp = 10 * self.gradient_penalty(images, gen, b, draw) * 5
+            gp.backward()
+        self.opt_D.step()
+        return real_loss, fake_loss, gp, r1, r2
 
 
 class Draw:

@@ -32,6 +32,8 @@ _KIND = {
     ("StyleConv", "scale_noise"): "noise_scale",
     ("StyleConv", "bias"): "style_bias",        # a no-op in the reference (generator_13_5.py:263)
     ("Smooth", "kernel"): "smooth",             # frozen binomial kernel, requires_grad=False
+    ("Conv2d", "weight"): "eqw",                # progan D: nn.Conv2d inside EqualizedConv2d, N(0,1) init
+                                                # (discriminator_3_wgangp_progan.py:20-24)
 }
 
 

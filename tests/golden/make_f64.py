@@ -151,7 +151,107 @@ def main():
     np.savez_compressed(os.path.join(HERE, "f64_truth.npz"), **out)
 
 
+def lazy_main(trials=4):
+    """Float64 truth of the two lazy-GP + R1/R2 critic steps of tests/golden/make_golden_lazy.py
+    (idx 0: with the regularisers, idx 1: without), the reference's distance to it, and the fp32
+    spread (weights perturbed by ~1 ulp)."""
+    torch.set_num_threads(os.cpu_count() or 8)
+    pl = plan()
+    fx = fixture("lazy_b4.npz")
+    dnames = [n for n, _, _ in pl["d_params"]]
+    out = {}
+    for idx, img_seed, rng_seed in ((0, 500, 501), (1, 510, 511)):
+        images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed))
+        smooth32 = om._SMOOTH
+        om._SMOOTH = smooth32.to(DT)
+        GP, DP = params64(pl["g_params"], pl["g_seed"]), params64(pl["d_params"], pl["d_seed"])
+        tr = om.WGANLazyR2(GP, DP)
+        losses = [float(v.detach().reshape(-1)[0])
+                  for v in tr.discriminator_trainstep(images.to(DT), 4, idx, Draw64(rng_seed))]
+        om._SMOOTH = smooth32
+        k = f"d{idx}"
+        out[f"{k}_losses"], out[f"{k}_grads"] = np.asarray(losses), grad_rows(DP, dnames)
+        out[f"ref_{k}_stats"] = np.asarray(grad_norm_stats(fx[f"{k}_grads"], out[f"{k}_grads"]))
+        n = 5 if idx == 0 else 2
+        out[f"ref_{k}_loss_err"] = np.asarray(rel_err(fx[f"{k}_losses"][:n], losses[:n]))
+        print("lazy truth", k, out[f"ref_{k}_stats"], out[f"ref_{k}_loss_err"], flush=True)
+        spread = []
+        for t in range(1, trials + 1):
+            GP = om.params_from_plan(pl["g_params"], pl["g_seed"])
+            DP = om.params_from_plan(pl["d_params"], pl["d_seed"])
+            g = torch.Generator().manual_seed(t)
+            with torch.no_grad():
+                for v in list(GP.t.values()) + list(DP.t.values()):
+                    v.mul_(1 + 6e-8 * torch.randn(v.shape, generator=g))
+            om.WGANLazyR2(GP, DP).discriminator_trainstep(images, 4, idx, om.Draw(rng_seed))
+            spread.append(grad_norm_stats(grad_rows(DP, dnames), out[f"{k}_grads"]))
+            print("lazy spread", k, t, spread[-1], flush=True)
+        out[f"{k}_fp32_spread"] = np.asarray(spread)
+    np.savez_compressed(os.path.join(HERE, "f64_lazy.npz"), **out)
+
+
+def progan_main(trials=6):
+    """Float64 truth of the progan pair's critic and generator steps (tests/golden/
+    make_golden_progan.py), the reference's distance to it, and the fp32 spread."""
+    import json
+    torch.set_num_threads(os.cpu_count() or 8)
+    with open(os.path.join(HERE, "plan_progan.json")) as f:
+        pp = json.load(f)
+    fx = fixture("progan_b4.npz")
+    dn = [n for n, _, _ in pp["d_params"]]
+    gn = [n for n, _, _ in pp["g_params"]]
+    images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(710))
+
+    def run(dt, perturb=None):
+        if dt == DT:
+            GP, DP = params64(pp["g_params"], pp["g_seed"]), params64(pp["d_params"], pp["d_seed"])
+            dr, dg = Draw64(711), Draw64(721)
+        else:
+            GP = om.params_from_plan(pp["g_params"], pp["g_seed"])
+            DP = om.params_from_plan(pp["d_params"], pp["d_seed"])
+            dr, dg = om.Draw(711), om.Draw(721)
+            g = torch.Generator().manual_seed(perturb)
+            with torch.no_grad():
+                for v in list(GP.t.values()) + list(DP.t.values()):
+                    v.mul_(1 + 6e-8 * torch.randn(v.shape, generator=g))
+        tr = om.WGANGP(GP, DP, gen=om.progan_generator, disc=om.progan_discriminator)
+        losses = [float(v.detach()) for v in tr.discriminator_trainstep(images.to(dt), 4, dr)]
+        drows = grad_rows(DP, dn)
+        GP2 = params64(pp["g_params"], pp["g_seed"]) if dt == DT else om.params_from_plan(pp["g_params"], pp["g_seed"])
+        DP2 = params64(pp["d_params"], pp["d_seed"]) if dt == DT else om.params_from_plan(pp["d_params"], pp["d_seed"])
+        if dt != DT:
+            g = torch.Generator().manual_seed(perturb)
+            with torch.no_grad():
+                for v in list(GP2.t.values()) + list(DP2.t.values()):
+                    v.mul_(1 + 6e-8 * torch.randn(v.shape, generator=g))
+        tr = om.WGANGP(GP2, DP2, gen=om.progan_generator, disc=om.progan_discriminator)
+        _gen, g_loss = tr.generator_trainstep(4, dg)
+        return losses + [float(g_loss.detach())], drows, grad_rows(GP2, gn)
+
+    losses, drows, grows = run(DT)
+    out = {"losses": np.asarray(losses), "d_grads": drows, "g_grads": grows,
+           "ref_d_stats": np.asarray(grad_norm_stats(fx["d_grads"], drows)),
+           "ref_g_stats": np.asarray(grad_norm_stats(fx["g_grads"], grows)),
+           "ref_loss_err": np.asarray(rel_err(np.r_[fx["d_losses"], fx["g_loss"]], losses))}
+    print("progan truth", out["ref_d_stats"], out["ref_g_stats"], out["ref_loss_err"], flush=True)
+    sd, sg, sl = [], [], []
+    for t in range(1, trials + 1):
+        l32, d32, g32 = run(torch.float32, perturb=t)
+        sd.append(grad_norm_stats(d32, drows))
+        sg.append(grad_norm_stats(g32, grows))
+        sl.append(rel_err(l32, losses))
+        print("progan spread", t, sd[-1], sg[-1], sl[-1], flush=True)
+    out["d_fp32_spread"], out["g_fp32_spread"], out["loss_fp32_spread"] = np.asarray(sd), np.asarray(sg), np.asarray(sl)
+    np.savez_compressed(os.path.join(HERE, "f64_progan.npz"), **out)
+
+
 if __name__ == "__main__":
+    if "--progan" in sys.argv:
+        progan_main()
+        sys.exit(0)
+    if "--lazy" in sys.argv:
+        lazy_main()
+        sys.exit(0)
     if "--spread-only" in sys.argv:     # add/refresh only the fp32 spread entry
         torch.set_num_threads(os.cpu_count() or 8)
         path = os.path.join(HERE, "f64_truth.npz")

@@ -1,0 +1,55 @@
+"""CPU: checkpoint save / resume (train/trainunits.py:58-130 naming and fields; state_dicts keyed
+by the reference's names; in-place load keeps the optimizers bound; optimizer state round trip)."""
+import json
+import os
+
+import torch
+
+import gan_amd
+from tests._util import GOLDEN
+
+
+def _trainer(tmp_path):
+    with open(os.path.join(GOLDEN, "plan_progan.json")) as f:
+        pp = json.load(f)
+    torch.manual_seed(0)
+    G = gan_amd.generator_3_progan.Generator(1, 256, pp["ngf"], 3)
+    D = gan_amd.discriminator_3_wgangp_progan.Discriminator(1, pp["ndf"], 3)
+    tr = gan_amd.Train([0] * 7, "cpu", 1, 256, G, "G3", D, "D3")
+    tr.ckpt_root = str(tmp_path / "checkpoint")
+    return pp, tr
+
+
+def test_checkpoint_round_trip(tmp_path):
+    pp, tr = _trainer(tmp_path)
+    tr.epoch, tr.i = 2, 5
+    with torch.no_grad():
+        tr.optimizer_D.exp_avg.normal_()
+        tr.optimizer_D.step_count.fill_(3)
+    path = tr.save_ckpt("WGANGP", 1, 4)
+    # reference naming and epoch/i carry: epoch + self.epoch + (i + self.i) // len, (i + self.i) % len
+    assert os.path.basename(path) == "G3 D3 WGANGP epoch_4 i_2_ckpt.pth"
+    ck = torch.load(path, weights_only=True)
+    assert (ck["generator_name"], ck["discriminator_name"], ck["method"], ck["epoch"], ck["i"]) == \
+        ("G3", "D3", "WGANGP", 4, 2)
+    # state_dict keys are the reference's parameter + buffer names
+    assert list(ck["generator"]) == [n for n, _ in tr.generator.state_dict().items()]
+    assert {n for n, _, _ in pp["g_params"]} | set(pp["g_buffers"]) == set(ck["generator"])
+    assert {n for n, _, _ in pp["d_params"]} == set(ck["discriminator"])
+    want_g = {k: v.clone() for k, v in tr.generator.state_dict().items()}
+    want_m = tr.optimizer_D.exp_avg.clone()
+    flat_ptr = tr.optimizer_G.flat.data.data_ptr()
+    with torch.no_grad():
+        for p in tr.generator.parameters():
+            p.add_(1.0)
+        tr.optimizer_D.exp_avg.zero_()
+    os.replace(path, os.path.join(tr.ckpt_root, "resume.pth"))
+    assert tr.load_generator_ckpt("resume") and tr.load_discriminator_ckpt("resume")
+    got = tr.generator.state_dict()
+    assert all(torch.equal(got[k], v) for k, v in want_g.items())
+    assert torch.equal(tr.optimizer_D.exp_avg, want_m) and int(tr.optimizer_D.step_count) == 3
+    # loaded in place: parameters are still views of the optimizer's flat buffer
+    assert all(p.data_ptr() >= flat_ptr for p in tr.generator.parameters())
+    assert tr.optimizer_G.flat.data.data_ptr() == flat_ptr
+    assert (tr.epoch, tr.i) == (4, 2)
+    assert not tr.load_generator_ckpt("missing")

@@ -183,3 +183,113 @@ def test_d_segments_equal_separate_calls(gan, P):
         both = D(torch.cat([a, b]), segments=2)
         assert rel_err(both.cpu().numpy(), sep.cpu().numpy()) < 1e-5
         assert rel_err(D(a).cpu().numpy(), sep[:8].cpu().numpy()) == 0   # segments reset to 1
+
+
+@pytest.mark.parametrize("idx,img_seed,rng_seed", [(0, 500, 501), (1, 510, 511)])
+def test_lazy_d_step(gan, P, idx, img_seed, rng_seed):
+    """Lazy GP + R1/R2 critic step (train/wganlazygpR2.py:48-77; Adam of trainunits.py:19) vs the
+    reference's fixture (tests/golden/make_golden_lazy.py) and float64 truth."""
+    fx = fixture("lazy_b4.npz")
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(rng_seed, DEV))
+    images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed)).to(DEV)
+    names = [n for n, _, _ in P["d_params"]]
+    before = {n: p.detach().clone() for n, p in D.named_parameters()}
+    losses = [float(v.detach().reshape(-1)[0]) for v in tr.discriminator_trainstep(images, 4, idx)]
+    want = fx[f"d{idx}_losses"]
+    # losses at the north-star 1e-3: the fake loss inherits the G13_5 output's fp32 error (the
+    # reference's own output is 2e-4 from float64 truth, test_oracle_golden::test_reference_fp32_error)
+    if idx == 0:
+        assert rel_err(losses, want) < 1e-3, (losses, want)
+        assert [k for k, _ in tr.rng.log][-1] == "rand"        # eps drawn after z and the noise
+    else:
+        assert rel_err(losses[:2], want[:2]) < 1e-3 and losses[2:] == [0.0, 0.0, 0.0]
+        assert "rand" not in [k for k, _ in tr.rng.log]
+    rows = _rows(D, names)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx[f"d{idx}_has_grad"]).all()
+    # the fake batch carries the G13_5 forward's fp32 error (BatchNorm1d over B=4) into every
+    # critic gradient, and R1/R2/GP add the double backward's conditioning: bar against float64
+    # truth (tests/golden/make_f64.py --lazy), 2x what fp32 itself reaches, as test_d_step does
+    k = f"d{idx}"
+    t64 = fixture("f64_lazy.npz")
+    check_vs_truth(rows, t64[f"{k}_grads"], t64[f"ref_{k}_stats"], t64[f"{k}_fp32_spread"])
+    n = 5 if idx == 0 else 2
+    assert rel_err(losses[:n], t64[f"{k}_losses"][:n]) < 1e-3
+    params = dict(D.named_parameters())
+    dl = np.asarray([tensor_summary((params[n].detach() - before[n]) / 4e-4)[1] for n in names])
+    ok = ~np.isnan(fx[f"d{idx}_deltas"][:, 1])
+    assert rel_err(dl[ok], fx[f"d{idx}_deltas"][ok, 1]) < 2e-3
+
+
+def test_lazy_g_step(gan, P):
+    """The generator step is wgangp.py's (its gradients are held to float64 truth by
+    test_g_step); what differs is the optimizer: Adam, lr 1e-4, betas (0.5, 0.99), no weight
+    decay (trainunits.py:18).  Step 1 of Adam moves each weight by ~lr*sign(g), so the per-tensor
+    update norms are robust to the G-step's fp32 conditioning and pin the optimizer."""
+    fx = fixture("lazy_b4.npz")
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(601, DEV))
+    names = [n for n, _, _ in P["g_params"]]
+    before = {n: p.detach().clone() for n, p in G.named_parameters()}
+    _gen, g_loss = tr.generator_trainstep(4)
+    assert rel_err([float(g_loss.detach())], fx["g_loss"]) < 1e-3
+    params = dict(G.named_parameters())
+    dl = np.asarray([tensor_summary((params[n].detach() - before[n]) / 1e-4)[1] for n in names])
+    ok = ~np.isnan(fx["g_deltas"][:, 1])
+    assert rel_err(dl[ok], fx["g_deltas"][ok, 1]) < 2e-3
+    assert tr.optimizer_G.betas == (0.5, 0.99) and tr.optimizer_G.weight_decay == 0.0
+
+
+# ---- progan pair under WGAN-GP (config 5) -----------------------------------------------------
+
+def _progan_pair(gan):
+    import json
+    import os
+    from tests._util import GOLDEN
+    with open(os.path.join(GOLDEN, "plan_progan.json")) as f:
+        pp = json.load(f)
+    G = gan.generator_3_progan.Generator(1, 256, pp["ngf"], 3)
+    D = gan.discriminator_3_wgangp_progan.Discriminator(1, pp["ndf"], 3)
+    fill_module(G, pp["g_seed"])
+    fill_module(D, pp["d_seed"])
+    return pp, G.to(DEV), D.to(DEV)
+
+
+def test_progan_forward(gan):
+    fx = fixture("progan_b4.npz")
+    pp, G, D = _progan_pair(gan)
+    with torch.no_grad():
+        g = G(torch.from_numpy(fx["z"]).to(DEV))
+        d = D(torch.from_numpy(fx["x"]).to(DEV))
+    assert tuple(g.shape) == (4, 3, 64, 64) and tuple(d.shape) == (4, 1)
+    assert rel_err(g.cpu().numpy(), fx["g_out"]) < 1e-4
+    assert rel_err(d.cpu().numpy(), fx["d_out"]) < 1e-4
+    buf = np.asarray([[float(b.double().sum()), float(b.double().norm())] for _, b in G.named_buffers()])
+    assert rel_err(buf, fx["g_buffers"]) < 1e-4
+
+
+def test_progan_steps(gan):
+    """One critic step (GP double backward) and one generator step vs the reference's fixture
+    (losses at the north-star 1e-3) and float64 truth (gradients within 2x the fp32 spread,
+    tests/golden/make_f64.py --progan)."""
+    fx = fixture("progan_b4.npz")
+    t64 = fixture("f64_progan.npz")
+    pp, G, D = _progan_pair(gan)
+    tr = gan.Train([0] * 10, DEV, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan.ReplayRNG(711, DEV))
+    images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(710)).to(DEV)
+    names = [n for n, _, _ in pp["d_params"]]
+    before = {n: p.detach().clone() for n, p in D.named_parameters()}
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, 4)]
+    assert rel_err(losses, fx["d_losses"]) < 1e-3, (losses, fx["d_losses"])
+    check_vs_truth(_rows(D, names), t64["d_grads"], t64["ref_d_stats"], t64["d_fp32_spread"])
+    params = dict(D.named_parameters())
+    dl = np.asarray([tensor_summary((params[n].detach() - before[n]) / 4e-4)[1] for n in names])
+    assert rel_err(dl, fx["d_deltas"][:, 1]) < 2e-3
+    pp, G, D = _progan_pair(gan)
+    tr = gan.Train([0] * 10, DEV, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan.ReplayRNG(721, DEV))
+    gen, g_loss = tr.generator_trainstep(4)
+    assert rel_err([float(g_loss.detach())], fx["g_loss"]) < 1e-3
+    assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-4
+    check_vs_truth(_rows(G, [n for n, _, _ in pp["g_params"]]), t64["g_grads"], t64["ref_g_stats"],
+                   t64["g_fp32_spread"])

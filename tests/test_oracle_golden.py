@@ -142,3 +142,99 @@ def test_reference_fp32_error(P):
         om._SMOOTH = smooth32
     err = rel_err(out.numpy(), fx["out"])
     assert 5e-5 < err < 1e-3, err
+
+
+def _step_rows(P, order, before=None, lr=None):
+    rows, deltas = [], []
+    for n in order:
+        t = P.t.get(n)
+        if t is not None and t.grad is not None:
+            rows.append(tensor_summary(t.grad))
+            if before is not None:
+                deltas.append(tensor_summary((t.detach() - before[n]) / lr)[1])
+        else:
+            rows.append([np.nan] * 11)
+            if before is not None:
+                deltas.append(np.nan)
+    return rows, np.asarray(deltas)
+
+
+@pytest.mark.parametrize("idx,img_seed,rng_seed", [(0, 500, 501), (1, 510, 511)])
+def test_lazy_d_step(P, idx, img_seed, rng_seed):
+    """Lazy GP + R1/R2 critic step (train/wganlazygpR2.py:48-77) vs the reference's fixture."""
+    fx = fixture("lazy_b4.npz")
+    GP, DP = _g(P), _d(P)
+    tr = om.WGANLazyR2(GP, DP)
+    images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed))
+    before = {k: v.detach().clone() for k, v in DP.t.items()}
+    losses = [float(v.detach().reshape(-1)[0]) for v in tr.discriminator_trainstep(images, 4, idx, om.Draw(rng_seed))]
+    want = fx[f"d{idx}_losses"]
+    if idx == 0:
+        assert rel_err(losses, want) < 1e-4
+    else:
+        assert rel_err(losses[:2], want[:2]) < 1e-4 and losses[2:] == [0.0, 0.0, 0.0]
+    rows, dl = _step_rows(DP, [n for n, k, _ in P["d_params"]], before, 4e-4)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx[f"d{idx}_has_grad"]).all()
+    check_grads(rows, fx[f"d{idx}_grads"], D_BAR)
+    ok = ~np.isnan(fx[f"d{idx}_deltas"][:, 1]) & ~np.isnan(dl)
+    assert rel_err(dl[ok], fx[f"d{idx}_deltas"][ok, 1]) < 1e-3
+
+
+def test_lazy_g_step(P):
+    """Same generator step as wgangp.py (test_g_step pins its gradients); what differs is the
+    optimizer (Adam, betas (0.5, 0.99), no decay), pinned by the per-tensor update norms (step 1
+    of Adam moves each weight by ~lr*sign(g): robust to the G-step's fp32 conditioning, which
+    moves the gradient norms by ~1e-3 between thread counts)."""
+    fx = fixture("lazy_b4.npz")
+    GP, DP = _g(P), _d(P)
+    tr = om.WGANLazyR2(GP, DP)
+    order = [n for n, k, _ in P["g_params"]]
+    before = {k: v.detach().clone() for k, v in GP.t.items()}
+    _gen, g_loss = tr.generator_trainstep(4, om.Draw(601))
+    assert rel_err([float(g_loss)], fx["g_loss"]) < 1e-4
+    _, dl = _step_rows(GP, order, before, 1e-4)
+    ok = ~np.isnan(fx["g_deltas"][:, 1]) & ~np.isnan(dl)
+    assert rel_err(dl[ok], fx["g_deltas"][ok, 1]) < 1e-3
+
+
+# ---- progan pair under WGAN-GP (config 5; tests/golden/make_golden_progan.py) ----------------
+
+def _progan():
+    import json
+    import os
+    from tests._util import GOLDEN
+    with open(os.path.join(GOLDEN, "plan_progan.json")) as f:
+        pp = json.load(f)
+    return pp, om.params_from_plan(pp["g_params"], pp["g_seed"]), om.params_from_plan(pp["d_params"], pp["d_seed"])
+
+
+def test_progan_forward():
+    fx = fixture("progan_b4.npz")
+    pp, GP, DP = _progan()
+    with torch.no_grad():
+        g = om.progan_generator(GP, torch.from_numpy(fx["z"]))
+        d = om.progan_discriminator(DP, torch.from_numpy(fx["x"]))
+    assert rel_err(g, fx["g_out"]) < 1e-5
+    assert rel_err(d, fx["d_out"]) < 1e-5
+    assert GP.used == {n for n, _, _ in pp["g_params"]} and DP.used == {n for n, _, _ in pp["d_params"]}
+
+
+def test_progan_steps():
+    fx = fixture("progan_b4.npz")
+    pp, GP, DP = _progan()
+    tr = om.WGANGP(GP, DP, gen=om.progan_generator, disc=om.progan_discriminator)
+    images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(710))
+    before = {k: v.detach().clone() for k, v in DP.t.items()}
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, 4, om.Draw(711))]
+    assert rel_err(losses, fx["d_losses"]) < 1e-4
+    rows, dl = _step_rows(DP, [n for n, _, _ in pp["d_params"]], before, 4e-4)
+    check_grads(rows, fx["d_grads"], D_BAR)
+    assert rel_err(dl, fx["d_deltas"][:, 1]) < 1e-3
+    pp, GP, DP = _progan()
+    tr = om.WGANGP(GP, DP, gen=om.progan_generator, disc=om.progan_discriminator)
+    gen, g_loss = tr.generator_trainstep(4, om.Draw(721))
+    assert rel_err([float(g_loss)], fx["g_loss"]) < 1e-4
+    assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-4
+    rows, _ = _step_rows(GP, [n for n, _, _ in pp["g_params"]])
+    check_grads(rows, fx["g_grads"], G_BAR)

@@ -62,3 +62,20 @@ def test_ell_roundtrip():
         for j in range(idx.shape[1]):
             dense[o, idx[o, j]] += w[o, j]
     assert np.allclose(dense, m, atol=1e-7)
+
+
+def test_progan_plan():
+    """Drop-in progan pair (config 5): module tree, parameter names / kinds / shapes / order and
+    buffers equal the reference's (tests/golden/plan_progan.json, made by importing it)."""
+    import json
+    import os
+    import gan_amd
+    from oracle.params import param_kinds
+    from tests._util import GOLDEN
+    with open(os.path.join(GOLDEN, "plan_progan.json")) as f:
+        pp = json.load(f)
+    G = gan_amd.generator_3_progan.Generator(1, 256, pp["ngf"], 3)
+    D = gan_amd.discriminator_3_wgangp_progan.Discriminator(1, pp["ndf"], 3)
+    assert [[n, k, list(s)] for n, k, s in param_kinds(G)] == pp["g_params"]
+    assert [[n, k, list(s)] for n, k, s in param_kinds(D)] == pp["d_params"]
+    assert [n for n, _ in G.named_buffers()] == pp["g_buffers"]
