@@ -41,6 +41,7 @@ class GTile(ctypes.Structure):
 # name -> (restype, argtypes)
 _SIGS = {
     "ganamd_version": (ctypes.c_char_p, []),
+    "ganamd_stream_capture_id": (c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_pack_bytes": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_pack": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, vp]),
@@ -120,6 +121,13 @@ def iptr(t):
 def workspace(nbytes: int, device) -> torch.Tensor:
     """Caller-provided scratch from torch's caching allocator (graph-capture safe)."""
     return torch.empty(max(int(nbytes), 4) // 4 + 1, dtype=torch.float32, device=device)
+
+
+def capture_id() -> int:
+    """Id of the HIP graph capture in progress on torch's current stream (0: not capturing)."""
+    v = ctypes.c_ulonglong(0)
+    check(LIB.ganamd_stream_capture_id(stream(), ctypes.byref(v)), "stream_capture_id")
+    return int(v.value)
 
 
 def version() -> str:

@@ -543,6 +543,15 @@ extern "C" {
 
 const char* ganamd_version(void) { return "ganamd 0.1 gfx950"; }
 
+int ganamd_stream_capture_id(hipStream_t stream, unsigned long long* capture_id) {
+  if (!capture_id) return GANAMD_EINVAL;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  if (hipStreamGetCaptureInfo(stream, &st, &id) != hipSuccess) return GANAMD_ELAUNCH;
+  *capture_id = st == hipStreamCaptureStatusActive ? id + 1 : 0;   // ids may start at 0
+  return GANAMD_OK;
+}
+
 size_t ganamd_rowreduce_workspace(int C, long L) {
   return sizeof(double) * 3 * (size_t)C * splits_for(L) + 2 * sizeof(float) * (size_t)C;
 }

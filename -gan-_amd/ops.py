@@ -137,7 +137,11 @@ class PackCache:
         root = w if w._base is None else w._base
         if not isinstance(root, torch.nn.Parameter):
             return None
-        key = (id(root), w.data_ptr(), geo.pack_key(op))
+        # A packed copy is only reused inside the execution context that made it: eager code, or
+        # ONE graph capture (its buffer lives in that graph's memory and is refreshed only when
+        # that graph replays).  A graph reading a copy packed by eager code or by another graph
+        # would see weights frozen at capture time, in memory the allocator may hand out again.
+        key = (id(root), w.data_ptr(), geo.pack_key(op), _lib.capture_id())
         # parameters living in an optimizer's flat buffer are stale only after THAT optimizer steps
         flat = getattr(root, "_gan_flat", None)
         epoch = (id(flat), flat.epoch) if flat is not None else cls.epoch

@@ -218,6 +218,8 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         iteration()
     torch.cuda.synchronize()
+    if rank == 0:
+        print(f"[bench] warm-up done ({args.config}, B={B}/GPU, {world} rank(s))", file=sys.stderr, flush=True)
 
     step = iteration
     graphs = {}
@@ -226,6 +228,12 @@ def main():
         # inside; torch advances the Philox offsets on every replay).  N = 1: backward + optimizer
         # in one graph.  N > 1: the RCCL all-reduce of the flat gradient runs eagerly between a
         # backward graph and an optimizer graph (collectives are kept out of capture).
+        # All phase graphs share ONE memory pool: the phases replay strictly one after another,
+        # so a later graph may reuse what an earlier one freed (per-graph pools would hold every
+        # phase's peak at once: > 250 GiB for the lazy config at B = 128).
+        pool = torch.cuda.graph_pool_handle()
+        torch.cuda.empty_cache()
+
         def capture(fn):
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -233,7 +241,7 @@ def main():
                 fn()
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, pool=pool):
                 fn()
             return g
 
@@ -245,6 +253,8 @@ def main():
             else:
                 graphs[key] = (capture(bwd), capture(opt.step), opt)
         torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] captured {len(graphs)} phase graphs", file=sys.stderr, flush=True)
 
         def step():
             for key, *_ in phases:
@@ -288,7 +298,8 @@ def main():
     if rank == 0 and world == 1 and headline and not args.no_extras:
         probe = roofline_probe(dev)
     if rank == 0:
-        print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
+        print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB "
+              f"(reserved {torch.cuda.max_memory_reserved() / 2**30:.1f}), "
               f"issued GEMM launches/iter {ops.FlopCounter.launches}", file=sys.stderr, flush=True)
         n_img = imgs_per_iter * world * args.steps
         t_iter = secs / args.steps

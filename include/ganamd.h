@@ -226,6 +226,11 @@ int ganamd_image_batch(const uint8_t* src, int B, int H, int W, const uint8_t* f
 /* Library identification (for load checks). */
 const char* ganamd_version(void);
 
+/* Capture state of a stream: *capture_id = the id of the HIP graph capture in progress on it, or
+ * 0 when the stream is not capturing.  Lets host-side caches of device buffers (packed weights)
+ * tell one graph capture from another and from eager execution. */
+int ganamd_stream_capture_id(hipStream_t stream, unsigned long long* capture_id);
+
 #ifdef __cplusplus
 }
 #endif
