@@ -13,7 +13,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_HERE, "libganamd.so")
+SO_PATH = os.environ.get("GANAMD_SO") or os.path.join(_HERE, "libganamd.so")   # GANAMD_SO: A/B builds
 
 c_int = ctypes.c_int
 c_long = ctypes.c_long
@@ -38,12 +38,22 @@ class GTile(ctypes.Structure):
                [("scale", ctypes.c_float)]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p)] + \
+               [(n, ctypes.c_int32) for n in ("sm", "sc", "st", "M", "Ck", "T", "Mpad", "Ckp")] + \
+               [("chunk0", ctypes.c_int64)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "ganamd_version": (ctypes.c_char_p, []),
     "ganamd_stream_capture_id": (c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
+    "ganamd_conv_plan_info": (c_int, [ctypes.POINTER(ConvDesc), c_int, c_int, ctypes.POINTER(ctypes.c_int)]),
     "ganamd_conv_pack_bytes": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
+    "ganamd_conv_pack_job": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, ctypes.POINTER(PackJob)]),
+    "ganamd_pack_job_chunks": (ctypes.c_int64, [ctypes.POINTER(PackJob)]),
+    "ganamd_conv_pack_batch": (c_int, [vp, c_int, ctypes.c_int64, vp]),
     "ganamd_conv_pack": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, vp]),
     "ganamd_conv_fwd_ex": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp, vp, vp, vp]),
     "ganamd_mix_fwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp]),

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -125,8 +126,11 @@ struct ConvArgs {
   const float* act;    // [M] or null: PReLU with these slopes, applied last
   float alpha;
   int N, ohw;          // N = B*OH*OW
-  int kt_per_split;
-  float* slab;         // split-K: per-split partial tiles [z][M][N] (null: single split)
+  // Block schedule (see ConvPlan): blocks [0, full_blocks) own whole tiles of the first nfull_t
+  // column tiles (m fastest); the remaining blocks split the K range of the tail tiles S ways.
+  int gy, full_blocks, nfull_t, S, kt_per_split;
+  int tail_n0, tail_cols;  // first tail column (pixel) and the tail width
+  float* slab;         // S > 1: per-split partial tail tiles [S][M][tail_cols]
 };
 
 struct WgradArgs {
@@ -198,14 +202,24 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
 // padded to the tile grid and to whole K-steps) so that every K-step of a row is 64 contiguous
 // bytes: one 16-byte buffer load per 4 k-values, no bounds tests.  The B operand is the
 // im2col/transposed gather; a thread owns one pixel n and KPT consecutive channels of the K-step.
+//
+// K order: channel chunk (BK channels) outer, tap inner -- k = (cc, t, c16).  All taps of one
+// chunk run back to back, so the gathered rows a block re-reads through the taps (16 channels x
+// its pixels + halo, ~13 KB) stay in L1/L2; tap-outer order would cycle every channel through
+// the cache between re-reads (the working set of the resident blocks of an XCD then exceeds
+// its 4 MB L2 on the 64-128-channel maps).
 __global__ void pack_a_kernel(const float* __restrict__ w, int sm, int sc, int st, int M, int Ck, int T, int Mpad,
                               int Ckp, float* __restrict__ out) {
   const long total = (long)Mpad * T * Ckp;
+  const int nct = Ckp / BK;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % Ckp);
-    const long r = i / Ckp;
+    const int c16 = (int)(i % BK);
+    const long r = i / BK;
     const int t = (int)(r % T);
-    const int m = (int)(r / T);
+    const long r2 = r / T;
+    const int cc = (int)(r2 % nct);
+    const int m = (int)(r2 / nct);
+    const int c = cc * BK + c16;
     out[i] = (m < M && c < Ck) ? w[(long)m * sm + (long)c * sc + (long)t * st] : 0.f;
   }
 }
@@ -222,12 +236,27 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int nct = p.Ckp / BK;
   const int kt_total = nct * p.T;
-  const int kt0 = blockIdx.z * p.kt_per_split;
-  const int kt1 = min(kt_total, kt0 + p.kt_per_split);
-  if (kt0 >= kt1) return;
+  int tx, ty, kt0, kt1, split = -1;
+  {
+    const int bid = blockIdx.x;
+    if (bid < p.full_blocks) {
+      ty = bid % p.gy;
+      tx = bid / p.gy;
+      kt0 = 0;
+      kt1 = kt_total;
+    } else {
+      const int t = bid - p.full_blocks;
+      const int r = t / p.S;
+      split = t - r * p.S;
+      ty = r % p.gy;
+      tx = p.nfull_t + r / p.gy;
+      kt0 = split * p.kt_per_split;
+      kt1 = min(kt_total, kt0 + p.kt_per_split);   // never empty: S = ceil(kt_total / kt_per_split)
+    }
+  }
+  const int n0 = tx * BN, m0 = ty * BM;
 
   // A slots: row m = slot/SPR, k = 4*(slot%SPR) (+ kt*BK): contiguous along the packed row
   constexpr int SPR = BK / 4;
@@ -259,13 +288,16 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 
   f32x4 ra[EA];
   float rb[KPT], rs[KPT];
-  // (t, cc): tap and channel chunk of the next K-step to load
-  int t = kt0 / nct, cc = kt0 - (kt0 / nct) * nct;
-  auto tap = [&](int tt) {
-    const int kh = tt / g.KW;
-    return n_ok ? tap_offset<MODE>(g, oh, ow, kh, tt - kh * g.KW) : -1;
-  };
-  int sp = tap(t);
+  // (cc, kh, kw): channel chunk and tap of the next K-step to load (k = (cc, t, c16))
+  int cc = kt0 / p.T;
+  int kh, kw;
+  {
+    const int t = kt0 - cc * p.T;
+    kh = t / g.KW;
+    kw = t - kh * g.KW;
+  }
+  auto tap = [&]() { return n_ok ? tap_offset<MODE>(g, oh, ow, kh, kw) : -1; };
+  int sp = tap();
 
   auto gload = [&](int kt) {
 #pragma unroll
@@ -280,10 +312,14 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
       rb[e] = bload(rx, (int)(base + (unsigned)e * cs4));
       if (BSCALE) rs[e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
     }
-    if (++cc == nct) {
-      cc = 0;
-      if (++t < p.T) sp = tap(t);
+    if (++kw == g.KW) {
+      kw = 0;
+      if (++kh * g.KW >= p.T) {
+        kh = 0;
+        ++cc;
+      }
     }
+    sp = tap();
   };
   auto sstore = [&](int buf) {
 #pragma unroll
@@ -320,8 +356,9 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
 
   // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // Split-K blocks store raw partial tiles to their slab; the reduce kernel applies the rest.
-  float* out = p.slab ? p.slab + (long)blockIdx.z * p.M * p.N : p.y;
-  const bool finish = p.slab == nullptr;
+  const bool finish = split < 0 || p.S == 1;
+  float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
+  const long ldo = finish ? p.N : p.tail_cols;
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
     const int n = n0 + (wn * C::TN + j) * 32 + (lane & 31);
@@ -340,9 +377,36 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
           if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.N + n];
           if (p.act) v = v > 0.f ? v : p.act[m] * v;
         }
-        out[(long)m * p.N + n] = v;
+        out[(long)m * ldo + n] = v;
       }
     }
+  }
+}
+
+// Batched repack: block b finds its job by binary search over the jobs' chunk offsets and packs
+// kPackChunk consecutive elements of that job's GEMM-order output.
+constexpr int kPackChunk = 4096;
+
+__global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* __restrict__ jobs, int n_jobs) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = n_jobs - 1;
+  while (lo < hi) {   // last job with chunk0 <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].chunk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const ganamd_pack_job j = jobs[lo];
+  const long total = (long)j.Mpad * j.T * j.Ckp;
+  const long i0 = (b - j.chunk0) * kPackChunk;
+  const int nct = j.Ckp / BK;
+  for (long i = i0 + threadIdx.x; i < min(total, i0 + kPackChunk); i += 256) {
+    const int c16 = (int)(i % BK);
+    const long r = i / BK;
+    const int t = (int)(r % j.T);
+    const long r2 = r / j.T;
+    const int cc = (int)(r2 % nct);
+    const int m = (int)(r2 / nct);
+    const int c = cc * BK + c16;
+    j.out[i] = (m < j.M && c < j.Ck) ? j.w[(long)m * j.sm + (long)c * j.sc + (long)t * j.st] : 0.f;
   }
 }
 
@@ -526,36 +590,34 @@ __global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict_
   }
 }
 
-// Input gradient of a small-map stride-1 conv from the per-tap products Z[(ci,t)][b,oh,ow]
-// (the "scatter" form of dgrad, see ganamd_conv_dgrad): every input pixel sums, per tap, the
-// outputs whose (padded) receptive field reads it -- one output per tap in the interior, a
-// run of outputs at a replication-padded edge.
+// Input gradient of a conv from the per-tap products Z[(ci,t)][b,oh,ow] (the "scatter" form of
+// dgrad, see ganamd_conv_dgrad): every input pixel sums, per tap, the outputs whose (padded)
+// receptive field reads it through that tap -- one output per tap in the interior (none for a
+// stride-2 tap of the wrong parity), a run of outputs at a replication-padded edge.  Input row i
+// is read by output row oh through tap kh iff clamp(oh*s - pad + kh) lies in [lo, hi], where
+// lo = hi = i, except that a replicated edge row also takes every position beyond the edge.
 __global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict__ gx, int C, int B, int H, int W,
-                                  int OH, int OW, int KH, int KW, int pad, int replicate) {
+                                  int OH, int OW, int KH, int KW, int stride, int pad, int replicate) {
   const long total = (long)C * B * H * W;
   const int T = KH * KW;
+  constexpr int kFar = 1 << 20;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int j = (int)(idx % W);
     const int i = (int)((idx / W) % H);
     const int b = (int)((idx / ((long)W * H)) % B);
     const int c = (int)(idx / ((long)W * H * B));
+    const int ilo = (replicate && i == 0) ? -kFar : i, ihi = (replicate && i == H - 1) ? kFar : i;
+    const int jlo = (replicate && j == 0) ? -kFar : j, jhi = (replicate && j == W - 1) ? kFar : j;
     float acc = 0.f;
     for (int kh = 0; kh < KH; ++kh) {
-      int h0 = i - kh + pad, h1 = h0;                       // outputs oh with pad-map(oh + kh - pad) == i
-      if (replicate) {
-        if (i == 0) h0 = 0;
-        if (i == H - 1) h1 = OH - 1;
-      }
-      h0 = max(h0, 0);
-      h1 = min(h1, OH - 1);
+      // oh*s in [ilo + pad - kh, ihi + pad - kh]
+      const int a0 = ilo + pad - kh, a1 = ihi + pad - kh;
+      const int h0 = max(0, a0 <= 0 ? 0 : (a0 + stride - 1) / stride);
+      const int h1 = min(OH - 1, a1 < 0 ? -1 : a1 / stride);
       for (int kw = 0; kw < KW; ++kw) {
-        int w0 = j - kw + pad, w1 = w0;
-        if (replicate) {
-          if (j == 0) w0 = 0;
-          if (j == W - 1) w1 = OW - 1;
-        }
-        w0 = max(w0, 0);
-        w1 = min(w1, OW - 1);
+        const int b0 = jlo + pad - kw, b1 = jhi + pad - kw;
+        const int w0 = max(0, b0 <= 0 ? 0 : (b0 + stride - 1) / stride);
+        const int w1 = min(OW - 1, b1 < 0 ? -1 : b1 / stride);
         const float* z = Z + ((long)(c * T + kh * KW + kw) * B + b) * OH * OW;
         for (int oh = h0; oh <= h1; ++oh)
           for (int ow = w0; ow <= w1; ++ow) acc += z[oh * OW + ow];
@@ -624,17 +686,163 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_
   return Plan{bm, bn, (kt_total + per - 1) / per, per};
 }
 
-Plan conv_plan(int M, int N, int Ck, int T) {
-  const int bm = conv_bm(M), bn = conv_bn(bm, N);
-  const int tiles = ((N + bn - 1) / bn) * ((M + bm - 1) / bm);
-  const int occ = bm == 64 ? 5 : 3;
-  return split_plan(bm, bn, tiles, ((Ck + BK - 1) / BK) * T, 2.0 * bm * bn * BK, (long)M * N, occ, 16, 4);
+// GANAMD_CONV_TILE=BMxBN forces a tile (experiments; e.g. 128x256, 256x128); 0/unset = heuristic.
+int conv_tile_override() {
+  static const int v = [] {
+    const char* e = getenv("GANAMD_CONV_TILE");
+    int a = 0, b = 0;
+    return (e && sscanf(e, "%dx%d", &a, &b) == 2) ? a * 1000 + b : 0;
+  }();
+  return v;
+}
+
+void conv_tile(int M, int* bm, int* bn) {
+  *bm = conv_bm(M);
+  *bn = conv_bn(*bm, 0);
+  if (const int o = conv_tile_override()) {
+    *bm = o / 1000;
+    *bn = o % 1000;
+  }
+}
+
+// Resident blocks per CU of a kernel instance (the runtime's occupancy calculator; without a
+// device -- CPU-only builds and ABI tests -- a conservative 2) and the CU count.
+int num_cus() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = kCUs;
+    return n;
+  }();
+  return v;
+}
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+int conv_occ() {
+  static const int v = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>, kThreads,
+                                                     0) != hipSuccess || n <= 0)
+      n = 2;
+    return n;
+  }();
+  return v;
+}
+
+template <int MODE, bool BSCALE>
+int conv_occ_tile(int bm, int bn) {
+  if (bm == 128 && bn == 256) return conv_occ<128, 256, 2, 2, MODE, BSCALE>();
+  if (bm == 256 && bn == 128) return conv_occ<256, 128, 2, 2, MODE, BSCALE>();
+  switch (bm) {
+    case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE>();
+    case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE>();
+    case 96: return conv_occ<96, 128, 1, 4, MODE, BSCALE>();
+    default: return conv_occ<128, 128, 2, 2, MODE, BSCALE>();
+  }
+}
+
+int conv_occupancy(int bm, int bn, int mode, bool bscale) {
+  switch (mode) {
+    case kZero: return bscale ? conv_occ_tile<kZero, true>(bm, bn) : conv_occ_tile<kZero, false>(bm, bn);
+    case kReplicate: return bscale ? conv_occ_tile<kReplicate, true>(bm, bn) : conv_occ_tile<kReplicate, false>(bm, bn);
+    default: return bscale ? conv_occ_tile<kTransposed, true>(bm, bn) : conv_occ_tile<kTransposed, false>(bm, bn);
+  }
+}
+
+// Conv GEMM block schedule.  A grid of gx x gy output tiles on `slots` resident blocks runs in
+// rounds; when the tile count is not a multiple of the slots the last round leaves most of the
+// chip idle (1024 tiles on 768 slots: 2 rounds for 1.33 rounds of work).  The plan keeps whole
+// tiles for the first nfull_t column tiles -- chosen so they fill whole rounds -- and splits the
+// K range of the remaining "tail" tiles S ways into extra blocks that fill the last round; their
+// partial sums go to slabs that conv_split_reduce_kernel folds (deterministic, no atomics).
+// nfull_t = 0 is plain split-K (small GEMMs), S = 1 no splitting.  The choice minimises the
+// makespan of greedy list scheduling of the blocks in dispatch order plus the reduce's cost.
+// A pure function of the geometry and the instance's occupancy (workspace query == launch).
+struct ConvPlan {
+  int bm, bn, gx, gy, nfull_t, S, kt_per_split;
+  long slab_elems;   // S > 1: S * M * tail_cols
+};
+
+constexpr double kSustainedTflops = 130.0;   // chip-wide fp32 MFMA rate of the GEMM body, all slots busy
+
+// Makespan (in K-steps of one block) of F equal blocks of length L followed by R equal blocks of
+// length d, list-scheduled in order on `slots` identical slots.
+double list_makespan(long F, double L, long R, double d, long slots) {
+  const long q = F / slots, r = F % slots;
+  const double a = q * L, b = (q + (r ? 1 : 0)) * L;   // (slots - r) slots free at a, r slots at b
+  if (R == 0) return b;
+  const long n1 = slots - r, n2 = r;
+  // smallest T (a breakpoint a + k d or b + k d) with n1 floor((T-a)/d) + n2 floor((T-b)/d) >= R
+  for (long k = 1;; ++k) {
+    const double T1 = a + k * d;
+    const long c1 = n1 * k + (T1 >= b + d ? n2 * (long)((T1 - b) / d + 1e-9) : 0);
+    if (c1 >= R) {
+      // the b-aligned breakpoint just below T1 may already suffice
+      const long kb = (long)((T1 - b) / d + 1e-9);
+      if (n2 && kb >= 1) {
+        const double T2 = b + kb * d;
+        if (T2 < T1 && n1 * (long)((T2 - a) / d + 1e-9) + n2 * kb >= R) return std::max(b, T2);
+      }
+      return std::max(b, T1);
+    }
+  }
+}
+
+ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale) {
+  ConvPlan pl{};
+  conv_tile(M, &pl.bm, &pl.bn);
+  pl.gx = (N + pl.bn - 1) / pl.bn;
+  pl.gy = (M + pl.bm - 1) / pl.bm;
+  const int kt_total = ((Ck + BK - 1) / BK) * T;
+  const long tiles = (long)pl.gx * pl.gy;
+  const long slots = (long)conv_occupancy(pl.bm, pl.bn, mode, bscale) * num_cus();
+  const double t_k = 2.0 * pl.bm * pl.bn * BK / (kSustainedTflops * 1e12 / slots) * 1e6;   // us per K-step
+  const double ovh = 1.0 / t_k;           // ~1 us per block of prologue / epilogue, in K-steps
+  auto cost = [&](int nf, int S, int* per_out) {
+    const int per = (kt_total + S - 1) / S;
+    const int Sx = (kt_total + per - 1) / per;   // no empty splits
+    const long F = (long)nf * pl.gy, R = (tiles - F) * Sx;
+    double c = list_makespan(F, kt_total + ovh, R, per + ovh, slots);
+    if (Sx > 1 && R > 0) {
+      const long tail_cols = N - (long)nf * pl.bn;
+      c += (3.0 + (2.0 * Sx + 1.0) * (double)M * tail_cols * 4.0 / 4e12 * 1e6) / t_k;
+    }
+    *per_out = per;
+    return c;
+  };
+  int best_nf = pl.gx, best_S = 1, per = kt_total;
+  double best = cost(pl.gx, 1, &per);
+  if (splitk_enabled()) {
+    const long q = tiles / slots;
+    int cand[4] = {0, (int)std::min<long>(pl.gx, q * slots / pl.gy), (int)std::min<long>(pl.gx, (q > 0 ? q - 1 : 0) * slots / pl.gy),
+                   pl.gx};
+    for (int nf : cand)
+      for (int S = 1; S <= 16 && kt_total / S >= 4; ++S) {
+        if (nf == pl.gx && S > 1) break;
+        int pp;
+        const double c = cost(nf, S, &pp);
+        if (c < best * 0.97) {   // deviate from whole tiles only for a clear win
+          best = c;
+          best_nf = nf;
+          best_S = S;
+        }
+      }
+  }
+  pl.nfull_t = best_nf;
+  const int pp = (kt_total + best_S - 1) / best_S;
+  pl.kt_per_split = pp;
+  pl.S = (kt_total + pp - 1) / pp;
+  const long tail_cols = std::max<long>(0, N - (long)pl.nfull_t * pl.bn);
+  pl.slab_elems = (pl.S > 1 && tail_cols > 0) ? (long)pl.S * M * tail_cols : 0;
+  return pl;
 }
 
 // bytes of the packed A operand of a conv GEMM (rows padded to the tile, K to whole K-steps)
 size_t pack_bytes(int M, int Ck, int T) {
-  const Plan pl = conv_plan(M, 1, Ck, T);   // bm depends on M only
-  const size_t mpad = (size_t)((M + pl.bm - 1) / pl.bm) * pl.bm;
+  int bm, bn;
+  conv_tile(M, &bm, &bn);
+  const size_t mpad = (size_t)((M + bm - 1) / bm) * bm;
   return sizeof(float) * mpad * T * (size_t)((Ck + BK - 1) / BK * BK);
 }
 
@@ -649,20 +857,23 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
   return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, 2.0 * bm * bn * BKW, (long)M * J * T, occ, 256, 4);
 }
 
-__global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int N, int ohw, int B,
-                                         const float* __restrict__ oscale, const float* __restrict__ bias,
-                                         const float* __restrict__ noise, const float* __restrict__ noise_scale,
-                                         const float* __restrict__ act, float* __restrict__ y) {
-  const long total = (long)M * N;
+// Folds the S partial slabs of the tail columns [n0, n0 + cols) and applies the epilogue.
+__global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int cols, int n0, int N,
+                                         int ohw, int B, const float* __restrict__ oscale,
+                                         const float* __restrict__ bias, const float* __restrict__ noise,
+                                         const float* __restrict__ noise_scale, const float* __restrict__ act,
+                                         float* __restrict__ y) {
+  const long total = (long)M * cols;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += slab[s * total + i];
-    const int m = (int)(i / N);
-    if (oscale) v *= oscale[m * B + (int)(i % N) / ohw];
+    const int m = (int)(i / cols);
+    const long o = (long)m * N + n0 + (i - (long)m * cols);
+    if (oscale) v *= oscale[m * B + (int)(o % N) / ohw];
     if (bias) v += bias[m];
-    if (noise) v += noise_scale[m] * noise[i];
+    if (noise) v += noise_scale[m] * noise[o];
     if (act) v = v > 0.f ? v : act[m] * v;
-    y[i] = v;
+    y[o] = v;
   }
 }
 
@@ -678,20 +889,29 @@ __global__ void wgrad_split_reduce_kernel(const float* __restrict__ slab, int S,
 int grid1d(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
 
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
-hipError_t launch_conv(ConvArgs p, const Plan& pl, float* slab, hipStream_t st) {
-  const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
+hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t st) {
+  p.gy = pl.gy;
+  p.nfull_t = pl.nfull_t;
+  p.full_blocks = pl.nfull_t * pl.gy;
+  p.S = pl.S;
   p.kt_per_split = pl.kt_per_split;
-  p.slab = pl.splits > 1 ? slab : nullptr;
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3(gx, gy, pl.splits), dim3(kThreads), 0,
+  p.tail_n0 = pl.nfull_t * BN;
+  p.tail_cols = std::max(0, p.N - p.tail_n0);
+  p.slab = pl.slab_elems ? slab : nullptr;
+  const long blocks = (long)p.full_blocks + (long)(pl.gx - pl.nfull_t) * pl.gy * pl.S;
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3((unsigned)blocks), dim3(kThreads), 0,
                      st, p);
-  if (pl.splits > 1)
-    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.N)), dim3(256), 0, st, slab, pl.splits,
-                       p.M, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act, p.y);
+  if (pl.slab_elems)
+    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.tail_cols)), dim3(256), 0, st, slab, pl.S,
+                       p.M, p.tail_cols, p.tail_n0, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
+                       p.y);
   return hipGetLastError();
 }
 
 template <int MODE, bool BSCALE>
-hipError_t dispatch_conv_tile(const ConvArgs& p, const Plan& pl, float* slab, hipStream_t st) {
+hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab, hipStream_t st) {
+  if (pl.bm == 128 && pl.bn == 256) return launch_conv<128, 256, 2, 2, MODE, BSCALE>(p, pl, slab, st);
+  if (pl.bm == 256 && pl.bn == 128) return launch_conv<256, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
   switch (pl.bm) {
     case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
@@ -708,8 +928,8 @@ void launch_pack(const ConvArgs& p, int mpad, int ckp, float* packed, hipStream_
 // p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
 // GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
-  const Plan pl = conv_plan(p.M, p.N, p.Ck, p.T);
-  if ((pl.splits > 1 && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
+  const ConvPlan pl = conv_plan(p.M, p.N, p.Ck, p.T, p.g.mode, p.g.scale != nullptr);
+  if ((pl.slab_elems && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
   const int mpad = (p.M + pl.bm - 1) / pl.bm * pl.bm;
   p.Ckp = (p.Ck + BK - 1) / BK * BK;
   if (!prepacked) {
@@ -784,12 +1004,13 @@ static void fwd_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T)
   *T = d->KH * d->KW;
 }
 
-// Small maps (<= 10x10), stride 1: dgrad as a plain GEMM over the conv's OUTPUT pixels,
+// Small maps (<= 10x10) and strided convs: dgrad as a plain GEMM over the conv's OUTPUT pixels,
 // Z[(ci,t)][n] = sum_co W[co][ci][t] * gy[co][n], then dgrad_fold_kernel.  The transposed
 // gather into the padded frame would feed the MFMAs mostly zero taps there (a 4x4 map's 6x6
-// frame: 2.25x the work; a valid 3x3 conv on 5x5: 2.8x).
+// frame: 2.25x the work; a valid 3x3 conv on 5x5: 2.8x; stride 2: 4x, three taps in four
+// have the wrong parity).  The Z round trip costs (KH*KW / stride^2) x the input gradient's bytes.
 static bool dgrad_scatter(const ganamd_conv_desc* d) {
-  return !d->transposed && d->stride == 1 && d->KH * d->KW > 1 && d->H * d->W <= 100;
+  return !d->transposed && d->KH * d->KW > 1 && (d->stride > 1 || d->H * d->W <= 100);
 }
 
 static void dgrad_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T) {
@@ -849,12 +1070,60 @@ static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// Gather mode of the fwd / dgrad GEMM; the split slabs the plan needs, for either scale variant
+// (the query does not know whether a scale will be passed; the launch plans with the actual one).
+static int fwd_mode(const ganamd_conv_desc* d) {
+  return d->transposed ? kTransposed : (d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero);
+}
+static int dgrad_mode(const ganamd_conv_desc* d) { return (dgrad_scatter(d) || d->transposed) ? kZero : kTransposed; }
+static size_t slab_bytes(int M, int N, int Ck, int T, int mode) {
+  const long a = conv_plan(M, N, Ck, T, mode, false).slab_elems, b = conv_plan(M, N, Ck, T, mode, true).slab_elems;
+  return sizeof(float) * (size_t)std::max(a, b);
+}
+
 int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes) {
   if (!desc_ok(d) || !bytes || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
   int M, Ck, T, sm, sc;
   a_operand(d, op, &M, &Ck, &T, &sm, &sc);
   *bytes = pack_bytes(M, Ck, T);
   return GANAMD_OK;
+}
+
+int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info) {
+  if (!desc_ok(d) || !info || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
+  int M, N, Ck, T;
+  if (op == GANAMD_CONV_FWD)
+    fwd_gemm(d, &M, &N, &Ck, &T);
+  else
+    dgrad_gemm(d, &M, &N, &Ck, &T);
+  const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
+  const ConvPlan pl = conv_plan(M, N, Ck, T, mode, scaled != 0);
+  const int v[10] = {pl.bm, pl.bn, pl.gx, pl.gy, pl.nfull_t, pl.S, pl.kt_per_split,
+                     pl.nfull_t * pl.gy + (pl.gx - pl.nfull_t) * pl.gy * pl.S, conv_occupancy(pl.bm, pl.bn, mode, scaled),
+                     num_cus()};
+  for (int i = 0; i < 10; ++i) info[i] = v[i];
+  return GANAMD_OK;
+}
+
+int ganamd_conv_pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed, ganamd_pack_job* job) {
+  if (!desc_ok(d) || !w || !packed || !job || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
+  int M, Ck, T, sm, sc, bm, bn;
+  a_operand(d, op, &M, &Ck, &T, &sm, &sc);
+  conv_tile(M, &bm, &bn);
+  *job = ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, (M + bm - 1) / bm * bm, (Ck + BK - 1) / BK * BK, 0};
+  return GANAMD_OK;
+}
+
+int64_t ganamd_pack_job_chunks(const ganamd_pack_job* job) {
+  if (!job) return 0;
+  const long total = (long)job->Mpad * job->T * job->Ckp;
+  return (total + kPackChunk - 1) / kPackChunk;
+}
+
+int ganamd_conv_pack_batch(const ganamd_pack_job* jobs, int n_jobs, int64_t total_chunks, hipStream_t stream) {
+  if (!jobs || n_jobs <= 0 || total_chunks <= 0 || total_chunks > 0x7fffffffL) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(pack_batch_kernel, dim3((unsigned)total_chunks), dim3(256), 0, stream, jobs, n_jobs);
+  return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 int ganamd_conv_pack(const ganamd_conv_desc* d, int op, const float* w, float* packed, hipStream_t stream) {
@@ -866,8 +1135,9 @@ int ganamd_conv_pack(const ganamd_conv_desc* d, int op, const float* w, float* p
   p.sm = sm;
   p.sc = sc;
   p.st = 1;
-  const Plan pl = conv_plan(p.M, 1, p.Ck, p.T);
-  launch_pack(p, (p.M + pl.bm - 1) / pl.bm * pl.bm, (p.Ck + BK - 1) / BK * BK, packed, stream);
+  int bm, bn;
+  conv_tile(p.M, &bm, &bn);
+  launch_pack(p, (p.M + bm - 1) / bm * bm, (p.Ck + BK - 1) / BK * BK, packed, stream);
   return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
@@ -877,14 +1147,11 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   *bytes = 0;
   if (op == GANAMD_CONV_FWD) {
     fwd_gemm(d, &M, &N, &Ck, &T);
-    const Plan pl = conv_plan(M, N, Ck, T);
-    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) +
-             (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + slab_bytes(M, N, Ck, T, fwd_mode(d));
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
-    const Plan pl = conv_plan(M, N, Ck, T);
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
-             align256(dgrad_scatter_bytes(d)) + (pl.splits > 1 ? sizeof(float) * (size_t)pl.splits * M * N : 0);
+             align256(dgrad_scatter_bytes(d)) + slab_bytes(M, N, Ck, T, dgrad_mode(d));
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
     T = d->KH * d->KW;
@@ -976,7 +1243,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
     const long total = (long)d->Cin * d->B * d->H * d->W;
     hipLaunchKernelGGL(dgrad_fold_kernel, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H, d->W,
-                       d->OH, d->OW, d->KH, d->KW, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
+                       d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
     return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   if (d->transposed) {

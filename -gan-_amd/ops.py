@@ -70,6 +70,16 @@ _DESC_CACHE: dict = {}
 _WS_CACHE: dict = {}
 
 
+PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus")
+
+
+def plan_info(geo: "Geo", op: int, scaled: bool = False) -> dict:
+    """The block schedule ganamd_conv_fwd / _dgrad launches for this geometry (ganamd_conv_plan_info)."""
+    info = (_lib.c_int * 10)()
+    check(LIB.ganamd_conv_plan_info(geo.desc(), op, int(scaled), info), "conv_plan_info")
+    return dict(zip(PLAN_FIELDS, list(info)))
+
+
 def conv_geo(B, cin, h, w, cout, k, stride=1, pad=0, pad_mode=_lib.PAD_REPLICATE):
     oh = (h + 2 * pad - k) // stride + 1
     ow = (w + 2 * pad - k) // stride + 1
@@ -116,9 +126,14 @@ class PackCache:
     changes.  A weight changes through (a) the fused optimizer, which bumps the epoch of its flat
     buffer (``FlatParams.epoch``; parameters outside one follow the global ``invalidate()``), or
     (b) torch in-place ops on the Parameter (``load_state_dict``, ``p.copy_``), which bump its
-    version counter.  Only weights that are Parameters (or views of one) are cached.  Under HIP
-    graph capture the pack launches are captured where the cache misses, so replays repack at
-    the same points."""
+    version counter.  Only weights that are Parameters (or views of one) are cached.
+
+    Weights living in an optimizer's flat buffer get a PERSISTENT copy (allocated eagerly, kept
+    for the life of the model) registered with that buffer (``PackRegistry``): the optimizer
+    refreshes every registered copy with one batched launch right after its update, so in the
+    steady state no conv call packs anything.  Other weights, and copies first needed inside a
+    HIP graph capture, are packed where the cache misses (under capture: captured there, so
+    replays repack at the same points; such a copy is only reused within that one capture)."""
 
     epoch = 0
     entries: dict = {}
@@ -133,27 +148,105 @@ class PackCache:
         cls.epoch += 1
 
     @classmethod
+    def _pack(cls, geo, op, w, packed):
+        check(LIB.ganamd_conv_pack(geo.desc(), op, ptr(w), ptr(packed), stream()), "conv_pack")
+
+    @classmethod
+    def _alloc(cls, geo, op, w):
+        n = _lib.c_size_t(0)
+        check(LIB.ganamd_conv_pack_bytes(geo.desc(), op, n), "conv_pack_bytes")
+        return torch.empty(n.value // 4, device=w.device, dtype=torch.float32)
+
+    @classmethod
     def get(cls, geo: "Geo", op: int, w):
         root = w if w._base is None else w._base
         if not isinstance(root, torch.nn.Parameter):
             return None
-        # A packed copy is only reused inside the execution context that made it: eager code, or
-        # ONE graph capture (its buffer lives in that graph's memory and is refreshed only when
-        # that graph replays).  A graph reading a copy packed by eager code or by another graph
-        # would see weights frozen at capture time, in memory the allocator may hand out again.
-        key = (id(root), w.data_ptr(), geo.pack_key(op), _lib.capture_id())
-        # parameters living in an optimizer's flat buffer are stale only after THAT optimizer steps
+        base_key = (id(root), w.data_ptr(), geo.pack_key(op))
         flat = getattr(root, "_gan_flat", None)
+        cap = _lib.capture_id()
+        if flat is not None:
+            reg = flat.packs
+            e = reg.entries.get(base_key)
+            if e is not None and e.root is root:
+                if e.version == root._version and reg.valid(e):
+                    return e.packed
+                if cap == 0:          # reloaded / modified in place: refresh this copy now
+                    cls._pack(geo, op, w, e.packed)
+                    e.version, e.epoch = root._version, flat.epoch
+                    return e.packed
+            elif cap == 0:            # first use: a persistent copy, refreshed by the optimizer
+                packed = cls._alloc(geo, op, w)
+                cls._pack(geo, op, w, packed)
+                reg.add(base_key, root, geo, op, w, packed, flat.epoch)
+                return packed
+        # A capture-local (or non-flat) copy: only reused inside the execution context that made
+        # it: eager code, or ONE graph capture (its buffer lives in that graph's memory and is
+        # refreshed only when that graph replays).
+        key = base_key + (cap,)
         epoch = (id(flat), flat.epoch) if flat is not None else cls.epoch
         e = cls.entries.get(key)
         if e is not None and e[0] is root and e[1] == root._version and e[2] == epoch:
             return e[3]
-        n = _lib.c_size_t(0)
-        check(LIB.ganamd_conv_pack_bytes(geo.desc(), op, n), "conv_pack_bytes")
-        packed = torch.empty(n.value // 4, device=w.device, dtype=torch.float32)
-        check(LIB.ganamd_conv_pack(geo.desc(), op, ptr(w), ptr(packed), stream()), "conv_pack")
+        packed = cls._alloc(geo, op, w)
+        cls._pack(geo, op, w, packed)
         cls.entries[key] = (root, root._version, epoch, packed)
         return packed
+
+
+class _PackEntry:
+    __slots__ = ("root", "version", "epoch", "packed", "job")
+
+    def __init__(self, root, version, epoch, packed, job):
+        self.root, self.version, self.epoch, self.packed, self.job = root, version, epoch, packed, job
+
+
+class PackRegistry:
+    """The persistent GEMM-order weight copies of one flat parameter buffer and the batched
+    repack (ganamd_conv_pack_batch) its optimizer launches after every update."""
+
+    def __init__(self, flat):
+        self.flat = flat
+        self.entries: dict = {}
+        self.table = None          # device copy of the job array
+        self.total_chunks = 0
+        self.dirty = False
+        self.batch_epoch = -1      # flat epoch at which the last batched repack was issued
+        self.retired = []
+
+    def add(self, key, root, geo, op, w, packed, epoch):
+        job = _lib.PackJob()
+        check(LIB.ganamd_conv_pack_job(geo.desc(), op, ptr(w), ptr(packed), job), "conv_pack_job")
+        self.entries[key] = _PackEntry(root, root._version, epoch, packed, job)
+        self.dirty = True
+
+    def valid(self, e) -> bool:
+        return e.epoch == self.flat.epoch or (self.batch_epoch == self.flat.epoch and e.epoch <= self.batch_epoch)
+
+    def repack(self):
+        """After the optimizer update (flat.epoch already bumped): refresh every copy, one launch."""
+        if not self.entries:
+            return
+        if self.dirty:
+            if _lib.capture_id():
+                raise _lib.GanAmdError("packed-weight table changed during graph capture (run one eager step first)")
+            jobs = (_lib.PackJob * len(self.entries))()
+            c0 = 0
+            for i, e in enumerate(self.entries.values()):
+                jobs[i] = e.job
+                jobs[i].chunk0 = c0
+                c0 += LIB.ganamd_pack_job_chunks(e.job)
+            raw = torch.frombuffer(bytearray(jobs), dtype=torch.uint8)
+            if self.table is not None:        # a captured graph may still launch with the old table
+                self.retired.append(self.table)
+            self.table = raw.to(self.flat.data.device)
+            self.total_chunks = c0
+            self.dirty = False
+        check(LIB.ganamd_conv_pack_batch(self.table.data_ptr(), len(self.entries), self.total_chunks, stream()),
+              "conv_pack_batch")
+        self.batch_epoch = self.flat.epoch
+        for e in self.entries.values():       # every copy now reflects the current weights
+            e.version, e.epoch = e.root._version, self.flat.epoch
 
 
 def invalidate_packed():

@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 
 from ._lib import LIB, check, iptr, ptr, stream
-from .ops import invalidate_packed
+from .ops import PackRegistry, invalidate_packed
 
 
 def _never_gets_grad(owner_cls: str, pname: str) -> bool:
@@ -54,6 +54,7 @@ class FlatParams:
             off += n
             p._gan_flat = self
         self.epoch = 0
+        self.packs = PackRegistry(self)   # persistent packed conv weights (ops.PackCache)
         invalidate_packed()
         module.__dict__["_flat"] = self      # lets the module find its flat buffers (style bank)
 
@@ -95,4 +96,5 @@ class FusedAdamW:
         check(LIB.ganamd_adamw(ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.n_train,
                                iptr(self.step_count), float(self.lr), float(self.betas[0]), float(self.betas[1]),
                                float(self.eps), float(self.weight_decay), stream()), "adamw")
-        f.epoch += 1   # packed conv weights of these parameters (ops.PackCache) are stale now
+        f.epoch += 1   # packed conv weights of these parameters (ops.PackCache) are stale now ...
+        f.packs.repack()   # ... until this one launch refreshes every registered copy

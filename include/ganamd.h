@@ -56,12 +56,33 @@ typedef struct ganamd_conv_desc {
 /* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD). */
 int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
 
+/* The block schedule conv_fwd / conv_dgrad will launch (introspection for tests and tools):
+ * info[10] = {BM, BN, column tiles, row tiles, whole-tile columns, tail K-splits, K-steps per
+ * split, blocks launched, resident blocks per CU of the instance, CUs}.  scaled: whether the
+ * x_scale / gy_scale operand will be passed (it selects the kernel instance). */
+int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info);
+
 /* The weight operand of conv_fwd / conv_dgrad in GEMM order (rows padded to the tile grid,
  * channels to whole K-steps, zero filled).  A caller that reuses a weight across calls (the
  * same parameter in forward, backward and the gradient penalty's double backward) packs it
  * once per optimizer step and passes packed_w = 1.  op: GANAMD_CONV_FWD or GANAMD_CONV_DGRAD. */
 int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes);
 int ganamd_conv_pack(const ganamd_conv_desc* d, int op, const float* w, float* packed, hipStream_t stream);
+
+/* Batched repack.  A model keeps one GEMM-order copy per (weight, op, geometry) it convolves
+ * with and refreshes ALL of them with one launch right after its optimizer step (instead of
+ * one pack launch per weight per step).  ganamd_conv_pack_job fills a job on the host (no GPU
+ * work); the caller sets chunk0 = the running sum of ganamd_pack_job_chunks over the preceding
+ * jobs, uploads the array, and launches ganamd_conv_pack_batch with the total chunk count. */
+typedef struct ganamd_pack_job {
+  const float* w;
+  float* out;
+  int32_t sm, sc, st, M, Ck, T, Mpad, Ckp;
+  int64_t chunk0;
+} ganamd_pack_job;
+int ganamd_conv_pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed, ganamd_pack_job* job);
+int64_t ganamd_pack_job_chunks(const ganamd_pack_job* job);
+int ganamd_conv_pack_batch(const ganamd_pack_job* jobs, int n_jobs, int64_t total_chunks, hipStream_t stream);
 
 /* y[co][b,oh,ow] = alpha * y_scale[co][b] * sum W * (x * x_scale[ci][b]) + bias[co]
  * Replaces: EqualizedConv2d.forward = F.conv2d(ReplicationPad2d(x), W*c, b)

@@ -246,8 +246,8 @@ def progan_main(trials=6):
 
 
 if __name__ == "__main__":
-    if "--progan" in sys.argv:
-        progan_main()
+    if "--progan" in sys.argv:   # --trials N: fp32 draws for the spread (default 6; the fixture uses 24)
+        progan_main(int(sys.argv[sys.argv.index("--trials") + 1]) if "--trials" in sys.argv else 6)
         sys.exit(0)
     if "--lazy" in sys.argv:
         lazy_main()

@@ -69,3 +69,33 @@ def test_python_wrappers_check_shapes(bad):
     w = torch.empty(4 * 3 * 9 + (1 if bad == "w" else 0))
     with pytest.raises(Exception):
         ops._conv_fwd(geo, x, w)
+
+
+@pytest.mark.parametrize("shape", [
+    # B, Cin, H, Cout, k, stride, pad: the census' large and small GEMMs
+    (128, 128, 32, 128, 3, 1, 1), (64, 96, 64, 96, 5, 1, 2), (64, 1025, 4, 1025, 3, 1, 1),
+    (64, 192, 5, 192, 3, 1, 1), (64, 1024, 16, 1024, 1, 1, 0), (64, 4100, 1, 4100, 1, 1, 0),
+    (128, 1024, 8, 1024, 3, 2, 1), (4, 5, 8, 7, 3, 1, 1)])
+@pytest.mark.parametrize("op", [0, 1])
+def test_conv_block_schedule(shape, op):
+    """Host-side invariants of the conv GEMM block schedule (whole tiles + K-split tail)."""
+    from gan_amd import _lib, ops
+    B, cin, h, cout, k, s, p = shape
+    geo = ops.conv_geo(B, cin, h, h, cout, k, s, p)
+    for scaled in (False, True):
+        pl = ops.plan_info(geo, op, scaled)
+        assert 0 <= pl["nfull_t"] <= pl["gx"] and pl["S"] >= 1
+        assert pl["blocks"] == pl["nfull_t"] * pl["gy"] + (pl["gx"] - pl["nfull_t"]) * pl["gy"] * pl["S"]
+        if pl["nfull_t"] == pl["gx"]:
+            assert pl["S"] == 1
+        # every split of a tail tile owns at least one K-step (no block leaves its slab unwritten)
+        nct = -(-(geo.Cout if op == 1 else geo.Cin) // 16)
+        taps = 1 if (op == 1 and (geo.stride > 1 or h * h <= 100) and k > 1) else k * k
+        kt_total = nct * taps
+        assert (pl["S"] - 1) * pl["kt_per_split"] < kt_total <= pl["S"] * pl["kt_per_split"]
+        n = _lib.c_size_t(0)
+        assert _lib.LIB.ganamd_conv_workspace(geo.desc(), op, n) == 0
+        if pl["S"] > 1:
+            tail_cols = (geo.B * (geo.OH * geo.OW if op == 0 else 1)) - pl["nfull_t"] * pl["bn"]
+            if op == 0:
+                assert n.value >= 4 * pl["S"] * geo.Cout * tail_cols
