@@ -24,12 +24,13 @@ vp = ctypes.c_void_p
 PAD_ZERO, PAD_REPLICATE = 0, 1
 EPI_STORE, EPI_BIAS, EPI_DEMOD, EPI_ACCUM, EPI_SCALE = 0, 1, 2, 3, 4
 CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
+MATH_F32, MATH_BF16 = 0, 1
 
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("B", "Cin", "H", "W", "Cout", "OH", "OW", "KH", "KW", "stride", "pad", "pad_mode", "transposed",
-                 "packed_w")]
+                 "packed_w", "math")]
 
 
 class GTile(ctypes.Structure):

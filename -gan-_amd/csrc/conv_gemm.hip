@@ -29,7 +29,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -38,6 +37,7 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -46,7 +46,13 @@ constexpr int kThreads = 256;
 #define GANAMD_BK 16
 #endif
 constexpr int BK = GANAMD_BK; // conv K-step (taps x channels)
+#ifdef GANAMD_LDS128
+// LDS row stride 20 floats: 16-byte aligned rows; ds_read_b128 (lane groups {0-3,12-15,20-27},
+// ...; bank (a/4) mod 64) and ds_write_b128 (8-lane groups, mod 32) are conflict-free at it.
+constexpr int LDK = BK + 4;
+#else
 constexpr int LDK = BK + 2;   // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
+#endif
 constexpr int BKW = 32;       // wgrad K-step (pixels): a half-wave reads one full 128-byte line
 constexpr int LDKW = BKW + 2;
 
@@ -131,6 +137,7 @@ struct ConvArgs {
   int gy, full_blocks, nfull_t, S, kt_per_split;
   int tail_n0, tail_cols;  // first tail column (pixel) and the tail width
   float* slab;         // S > 1: per-split partial tail tiles [S][M][tail_cols]
+  int bf16;            // GANAMD_MATH_BF16: operands rounded to bf16, fp32 accumulation
 };
 
 struct WgradArgs {
@@ -145,6 +152,7 @@ struct WgradArgs {
   int kt_per_split, splits, accumulate;
   float* slab;         // split-K: per-split partial weights [split][numel(out)] (null: single split)
   int out_numel;
+  int bf16;
 };
 
 template <int BM, int BN, int WGM, int WGN>
@@ -156,7 +164,19 @@ struct TileCfg {
 };
 
 // Read this lane's 8 k-values of one 32-row fragment: rows r of the [row][k] tile, k = 8h..8h+7.
+template <int LD>
 __device__ __forceinline__ void read_frag(const float* __restrict__ base, float (&v)[8]) {
+#ifdef GANAMD_LDS128
+  if constexpr (LD % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(base + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const f32x2 t = *reinterpret_cast<const f32x2*>(base + 2 * q);
@@ -167,15 +187,40 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 
 // One 16-deep K-step of MFMAs for a wave over LDS tiles of row stride LD, starting at column
 // k0.  In step s lane half h supplies k = k0 + 8h + s.
-template <class C, int LD = LDK>
+//
+// bf16 math (GANAMD_MATH_BF16, the bf16 configuration): the same LDS tiles and lane reads; the
+// lane's 8 k-values are rounded to bf16 (RNE) and ONE v_mfma_f32_32x32x16_bf16 replaces the 8
+// f32 steps -- its operand map is exactly this one (lane (r, h) holds A[r][8h + j] and
+// B[8h + j][r], j = 0..7) and its C/D map that of 32x32x2 f32, so nothing else changes.
+template <class C, int LD = LDK, bool BF16 = false>
 __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
-                                          f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0 = 0) {
+                                          f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0) {
   const int r = lane & 31, h = lane >> 5;
   float a[C::TM][8], b[C::TN][8];
 #pragma unroll
-  for (int i = 0; i < C::TM; ++i) read_frag(As + ((wm * C::TM + i) * 32 + r) * LD + k0 + 8 * h, a[i]);
+  for (int i = 0; i < C::TM; ++i) read_frag<LD>(As + ((wm * C::TM + i) * 32 + r) * LD + k0 + 8 * h, a[i]);
 #pragma unroll
-  for (int j = 0; j < C::TN; ++j) read_frag(Bs + ((wn * C::TN + j) * 32 + r) * LD + k0 + 8 * h, b[j]);
+  for (int j = 0; j < C::TN; ++j) read_frag<LD>(Bs + ((wn * C::TN + j) * 32 + r) * LD + k0 + 8 * h, b[j]);
+  if constexpr (BF16) {
+    bf16x8 av[C::TM], bv[C::TN];
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[i][e] = (__bf16)a[i][e];
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[j][e] = (__bf16)b[j][e];
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    return;
+  }
+#ifdef GANAMD_SETPRIO
+  __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
   for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -183,6 +228,9 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
 #pragma unroll
       for (int j = 0; j < C::TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+#ifdef GANAMD_SETPRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 template <class C>
@@ -224,7 +272,7 @@ __global__ void pack_a_kernel(const float* __restrict__ w, int sm, int sc, int s
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
 __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int A4 = BM * BK / 4;                      // 16-byte slots of the A tile
@@ -300,6 +348,9 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
   int sp = tap();
 
   auto gload = [&](int kt) {
+#ifdef GANAMD_EXP_NOLOAD   // timing experiment only: operands stop changing after the first K-steps
+    if (kt > kt0 + 1) return;
+#endif
 #pragma unroll
     for (int e = 0; e < EA; ++e)
       if (tid + e * kThreads < A4) ra[e] = bload4(rw, a_off[e] + kt * (BK * 4));
@@ -327,11 +378,25 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
       const int slot = tid + e * kThreads;
       if (slot < A4) {
         float* d = &As[buf][(slot / SPR) * LDK + 4 * (slot % SPR)];
+#ifdef GANAMD_LDS128
+        *reinterpret_cast<f32x4*>(d) = ra[e];
+#else
         *reinterpret_cast<f32x2*>(d) = f32x2{ra[e][0], ra[e][1]};
         *reinterpret_cast<f32x2*>(d + 2) = f32x2{ra[e][2], ra[e][3]};
+#endif
       }
     }
     float* d = &Bs[buf][b_n * LDK + b_kg * KPT];
+#ifdef GANAMD_LDS128
+    if constexpr (KPT % 4 == 0) {
+#pragma unroll
+      for (int e = 0; e < KPT; e += 4)
+        *reinterpret_cast<f32x4*>(d + e) =
+            BSCALE ? f32x4{rb[e] * rs[e], rb[e + 1] * rs[e + 1], rb[e + 2] * rs[e + 2], rb[e + 3] * rs[e + 3]}
+                   : f32x4{rb[e], rb[e + 1], rb[e + 2], rb[e + 3]};
+      return;
+    }
+#endif
 #pragma unroll
     for (int e = 0; e < KPT; e += 2)
       *reinterpret_cast<f32x2*>(d + e) =
@@ -349,7 +414,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
 #pragma unroll
-    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
+    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -371,6 +436,171 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
         float v = p.alpha * acc[i][j][r];
+        if (finish) {
+          if (p.oscale) v *= p.oscale[m * g.B + b];
+          if (p.bias) v += p.bias[m];
+          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.N + n];
+          if (p.act) v = v > 0.f ? v : p.act[m] * v;
+        }
+        out[(long)m * ldo + n] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Direct variant: no LDS, no barriers.  Each wave owns a (32*TM) x (32*TN) output tile and loads
+// its MFMA operands straight into registers: with the k-permuted 32x32x2 layout, lane (r, h)
+// needs A[row r][k = 8h .. 8h+7] (32 contiguous bytes of the packed weight row: two 16-byte
+// loads) and B[k = 8h .. 8h+7][pixel r] (8 channel rows of the gathered source at one pixel:
+// 8 dword loads, coalesced across the 32 pixels of a half-wave).  The operands of K-step kt+1
+// are loaded into a second register set while the MFMAs of K-step kt run, so the only waits are
+// the compiler's counted vmcnt on loads issued a whole K-step earlier; the 4 waves of a block
+// share the A rows (and the taps' overlapping pixels) through L1 instead of LDS.
+template <int TM, int TN, int MODE, bool BSCALE>
+__global__ __launch_bounds__(kThreads) void conv_direct_kernel(ConvArgs p) {
+  constexpr int BM = 32 * TM, BN = 4 * 32 * TN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nct = p.Ckp / BK;
+  const int kt_total = nct * p.T;
+  int tx, ty, kt0, kt1, split = -1;
+  {
+    const int bid = blockIdx.x;
+    if (bid < p.full_blocks) {
+      ty = bid % p.gy;
+      tx = bid / p.gy;
+      kt0 = 0;
+      kt1 = kt_total;
+    } else {
+      const int t = bid - p.full_blocks;
+      const int rr = t / p.S;
+      split = t - rr * p.S;
+      ty = rr % p.gy;
+      tx = p.nfull_t + rr / p.gy;
+      kt0 = split * p.kt_per_split;
+      kt1 = min(kt_total, kt0 + p.kt_per_split);
+    }
+  }
+  const int m0 = ty * BM;
+  const int nw0 = tx * BN + wave * (32 * TN);   // this wave's first pixel
+  const Gather& g = p.g;
+  const int Krow = p.T * p.Ckp;
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
+  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
+
+  // per fragment j: this lane's pixel
+  int img[TN], poh[TN], pow_[TN], pb[TN];
+  bool pok[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = nw0 + j * 32 + r;
+    pok[j] = n < p.N;
+    const int nn = pok[j] ? n : 0;
+    pb[j] = nn / p.ohw;
+    const int rr = nn - pb[j] * p.ohw;
+    poh[j] = rr / g.OW;
+    pow_[j] = rr - poh[j] * g.OW;
+    img[j] = pb[j] * g.H * g.W;
+  }
+  // A: row m0 + i*32 + r, k = kt*16 + 8h .. +7  (packed rows are padded to the tile grid)
+  int a_off[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) a_off[i] = 4 * ((m0 + i * 32 + r) * Krow + 8 * h);
+
+  int cc = kt0 / p.T, kh, kw;
+  {
+    const int t = kt0 - cc * p.T;
+    kh = t / g.KW;
+    kw = t - kh * g.KW;
+  }
+
+  f32x4 ra[2][TM][2];
+  float rb[2][TN][8], rs[2][TN][8];
+  auto gload = [&](int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ra[buf][i][0] = bload4(rw, a_off[i] + kt * (BK * 4));
+      ra[buf][i][1] = bload4(rw, a_off[i] + kt * (BK * 4) + 16);
+    }
+    const int c = cc * BK + 8 * h;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int sp = pok[j] ? tap_offset<MODE>(g, poh[j], pow_[j], kh, kw) : -1;
+      const unsigned base = sp >= 0 ? 4u * (unsigned)(img[j] + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
+      const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + pb[j]) : (unsigned)kOOB;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        rb[buf][j][e] = bload(rx, (int)(base + (unsigned)e * cs4));
+        if (BSCALE) rs[buf][j][e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
+      }
+    }
+    if (++kw == g.KW) {
+      kw = 0;
+      if (++kh * g.KW >= p.T) {
+        kh = 0;
+        ++cc;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  auto compute = [&](int buf) {
+    float a[TM][8], b[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[i][e] = ra[buf][i][0][e];
+        a[i][4 + e] = ra[buf][i][1][e];
+      }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[j][e] = BSCALE ? rb[buf][j][e] * rs[buf][j][e] : rb[buf][j][e];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  gload(kt0, 0);
+  int kt = kt0;
+  for (; kt + 2 <= kt1; kt += 2) {
+    gload(kt + 1, 1);
+    compute(0);
+    if (kt + 2 < kt1) gload(kt + 2, 0);
+    compute(1);
+  }
+  if (kt < kt1) compute(0);
+
+  const bool finish = split < 0 || p.S == 1;
+  float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
+  const long ldo = finish ? p.N : p.tail_cols;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = nw0 + j * 32 + r;
+    if (n >= p.N) continue;
+    const int b = (finish && p.oscale) ? n / p.ohw : 0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m >= p.M) continue;
+        float v = p.alpha * acc[i][j][q];
         if (finish) {
           if (p.oscale) v *= p.oscale[m * g.B + b];
           if (p.bias) v += p.bias[m];
@@ -413,7 +643,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
 // ------------------------------------------------------------------------------------------
 // wgrad: K = output pixels n, M = output channels of the conv, N = gathered channels at tap t
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED, bool BF16>
 __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int A4 = BM * BKW / 4;                     // 16-byte slots of the A tile (4 pixels of a row)
@@ -537,8 +767,8 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_tile<C, LDKW>(As[buf], Bs[buf], acc, lane, wm, wn, 0);
-    mfma_tile<C, LDKW>(As[buf], Bs[buf], acc, lane, wm, wn, 16);
+    mfma_tile<C, LDKW, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, 0);
+    mfma_tile<C, LDKW, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, 16);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -653,14 +883,18 @@ int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
 int conv_bn(int bm, int) { return bm == 32 ? 256 : 128; }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
 
-// Split-K by a small cost model: a GEMM of `tiles` output tiles, each `kt_total` K-steps of
-// `kflop` FLOPs, runs in ceil(tiles*s / slots) waves of blocks (slots = resident blocks per CU
-// x 256 CUs, from the compiler's resource report of the instance) of ceil(kt_total/s) K-steps;
-// splitting adds the slab round trip and a reduce launch.  Pure function of the geometry (the
-// workspace query and the launch agree).
+// Split-K: pure functions of the geometry (the workspace query and the launch agree).
 constexpr int kCUs = 256;
-constexpr double kBlockTflops = 110.0;   // measured sustained fp32 MFMA rate of the GEMM kernels
 
+int num_cus();
+double list_makespan(long F, double L, long R, double d, long slots);
+
+// wgrad split-K by a small cost model: a GEMM of `tiles` output tiles, each `kt_total` K-steps of
+// `kflop` FLOPs, runs in ceil(tiles*s / slots) rounds of blocks (slots = resident blocks per CU
+// x CUs) of ceil(kt_total/s) K-steps; splitting adds the slab round trip and a reduce launch.
+// (A CU-level "fluid" model -- one block alone runs at the CU's full rate -- was measured to
+// under-split the big-K wgrads 1.4-2x: a lone block of 4 waves does not fill its CU.)
+constexpr double kBlockTflops = 110.0;   // measured sustained fp32 MFMA rate of the GEMM kernels
 Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_elems, int occ, int max_splits,
                 int min_k) {
   const int slots = occ * kCUs;
@@ -686,23 +920,19 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_
   return Plan{bm, bn, (kt_total + per - 1) / per, per};
 }
 
-// GANAMD_CONV_TILE=BMxBN forces a tile (experiments; e.g. 128x256, 256x128); 0/unset = heuristic.
-int conv_tile_override() {
+// GANAMD_CONV_KERNEL=lds selects the LDS-staged kernel, =direct the LDS-free one (default).
+int conv_direct() {
   static const int v = [] {
-    const char* e = getenv("GANAMD_CONV_TILE");
-    int a = 0, b = 0;
-    return (e && sscanf(e, "%dx%d", &a, &b) == 2) ? a * 1000 + b : 0;
+    const char* e = getenv("GANAMD_CONV_KERNEL");
+    return (e && e[0] == 'd') ? 1 : 0;   // default: the LDS kernel (direct measured at parity or slower)
   }();
   return v;
 }
+constexpr int kDirectTN = 2;
 
 void conv_tile(int M, int* bm, int* bn) {
   *bm = conv_bm(M);
-  *bn = conv_bn(*bm, 0);
-  if (const int o = conv_tile_override()) {
-    *bm = o / 1000;
-    *bn = o % 1000;
-  }
+  *bn = conv_direct() ? 4 * 32 * kDirectTN : conv_bn(*bm, 0);
 }
 
 // Resident blocks per CU of a kernel instance (the runtime's occupancy calculator; without a
@@ -718,11 +948,11 @@ int num_cus() {
   return v;
 }
 
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
 int conv_occ() {
   static const int v = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>, kThreads,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, BF16>, kThreads,
                                                      0) != hipSuccess || n <= 0)
       n = 2;
     return n;
@@ -730,41 +960,61 @@ int conv_occ() {
   return v;
 }
 
-template <int MODE, bool BSCALE>
+template <int TM, int MODE, bool BSCALE>
+int direct_occ() {
+  static const int v = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_direct_kernel<TM, kDirectTN, MODE, BSCALE>, kThreads, 0) !=
+            hipSuccess || n <= 0)
+      n = 2;
+    return n;
+  }();
+  return v;
+}
+
+template <int MODE, bool BSCALE, bool BF16>
 int conv_occ_tile(int bm, int bn) {
-  if (bm == 128 && bn == 256) return conv_occ<128, 256, 2, 2, MODE, BSCALE>();
-  if (bm == 256 && bn == 128) return conv_occ<256, 128, 2, 2, MODE, BSCALE>();
+  if (conv_direct() && !BF16) {
+    switch (bm) {
+      case 32: return direct_occ<1, MODE, BSCALE>();
+      case 64: return direct_occ<2, MODE, BSCALE>();
+      case 96: return direct_occ<3, MODE, BSCALE>();
+      default: return direct_occ<4, MODE, BSCALE>();
+    }
+  }
   switch (bm) {
-    case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE>();
-    case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE>();
-    case 96: return conv_occ<96, 128, 1, 4, MODE, BSCALE>();
-    default: return conv_occ<128, 128, 2, 2, MODE, BSCALE>();
+    case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE, BF16>();
+    case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
+    case 96: return conv_occ<96, 128, 1, 4, MODE, BSCALE, BF16>();
+    default: return conv_occ<128, 128, 2, 2, MODE, BSCALE, BF16>();
   }
 }
 
-int conv_occupancy(int bm, int bn, int mode, bool bscale) {
+template <bool BF16>
+int conv_occupancy_t(int bm, int bn, int mode, bool bscale) {
   switch (mode) {
-    case kZero: return bscale ? conv_occ_tile<kZero, true>(bm, bn) : conv_occ_tile<kZero, false>(bm, bn);
-    case kReplicate: return bscale ? conv_occ_tile<kReplicate, true>(bm, bn) : conv_occ_tile<kReplicate, false>(bm, bn);
-    default: return bscale ? conv_occ_tile<kTransposed, true>(bm, bn) : conv_occ_tile<kTransposed, false>(bm, bn);
+    case kZero: return bscale ? conv_occ_tile<kZero, true, BF16>(bm, bn) : conv_occ_tile<kZero, false, BF16>(bm, bn);
+    case kReplicate:
+      return bscale ? conv_occ_tile<kReplicate, true, BF16>(bm, bn) : conv_occ_tile<kReplicate, false, BF16>(bm, bn);
+    default:
+      return bscale ? conv_occ_tile<kTransposed, true, BF16>(bm, bn) : conv_occ_tile<kTransposed, false, BF16>(bm, bn);
   }
 }
 
-// Conv GEMM block schedule.  A grid of gx x gy output tiles on `slots` resident blocks runs in
-// rounds; when the tile count is not a multiple of the slots the last round leaves most of the
-// chip idle (1024 tiles on 768 slots: 2 rounds for 1.33 rounds of work).  The plan keeps whole
-// tiles for the first nfull_t column tiles -- chosen so they fill whole rounds -- and splits the
-// K range of the remaining "tail" tiles S ways into extra blocks that fill the last round; their
-// partial sums go to slabs that conv_split_reduce_kernel folds (deterministic, no atomics).
-// nfull_t = 0 is plain split-K (small GEMMs), S = 1 no splitting.  The choice minimises the
-// makespan of greedy list scheduling of the blocks in dispatch order plus the reduce's cost.
-// A pure function of the geometry and the instance's occupancy (workspace query == launch).
+int conv_occupancy(int bm, int bn, int mode, bool bscale, bool bf16) {
+  return bf16 ? conv_occupancy_t<true>(bm, bn, mode, bscale) : conv_occupancy_t<false>(bm, bn, mode, bscale);
+}
+
+// Conv GEMM block schedule.  The plan keeps whole tiles for the first nfull_t column tiles and
+// splits the K range of the remaining "tail" tiles S ways into extra blocks; their partial sums
+// go to slabs that conv_split_reduce_kernel folds (deterministic, no atomics).  nfull_t = 0 is
+// plain split-K (small GEMMs), S = 1 no splitting.  The choice minimises the makespan of greedy
+// list scheduling of the blocks (in dispatch order, onto CUs) plus the reduce's cost.  A pure
+// function of the geometry (workspace query == launch).
 struct ConvPlan {
   int bm, bn, gx, gy, nfull_t, S, kt_per_split;
   long slab_elems;   // S > 1: S * M * tail_cols
 };
-
-constexpr double kSustainedTflops = 130.0;   // chip-wide fp32 MFMA rate of the GEMM body, all slots busy
 
 // Makespan (in K-steps of one block) of F equal blocks of length L followed by R equal blocks of
 // length d, list-scheduled in order on `slots` identical slots.
@@ -789,14 +1039,18 @@ double list_makespan(long F, double L, long R, double d, long slots) {
   }
 }
 
-ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale) {
+constexpr double kSustainedTflops = 130.0;   // chip-wide fp32 MFMA rate of the GEMM body, all slots busy
+
+ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {
   ConvPlan pl{};
   conv_tile(M, &pl.bm, &pl.bn);
   pl.gx = (N + pl.bn - 1) / pl.bn;
   pl.gy = (M + pl.bm - 1) / pl.bm;
   const int kt_total = ((Ck + BK - 1) / BK) * T;
   const long tiles = (long)pl.gx * pl.gy;
-  const long slots = (long)conv_occupancy(pl.bm, pl.bn, mode, bscale) * num_cus();
+  // slot-level model (blocks run in rounds of occupancy x CUs); the CU-level "fluid" model was
+  // measured 7 % slower over the iteration (it under-splits: a lone block does not fill its CU)
+  const long slots = (long)conv_occupancy(pl.bm, pl.bn, mode, bscale, bf16) * num_cus();
   const double t_k = 2.0 * pl.bm * pl.bn * BK / (kSustainedTflops * 1e12 / slots) * 1e6;   // us per K-step
   const double ovh = 1.0 / t_k;           // ~1 us per block of prologue / epilogue, in K-steps
   auto cost = [&](int nf, int S, int* per_out) {
@@ -888,7 +1142,7 @@ __global__ void wgrad_split_reduce_kernel(const float* __restrict__ slab, int S,
 
 int grid1d(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
 
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
 hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t st) {
   p.gy = pl.gy;
   p.nfull_t = pl.nfull_t;
@@ -899,7 +1153,7 @@ hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t 
   p.tail_cols = std::max(0, p.N - p.tail_n0);
   p.slab = pl.slab_elems ? slab : nullptr;
   const long blocks = (long)p.full_blocks + (long)(pl.gx - pl.nfull_t) * pl.gy * pl.S;
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE>), dim3((unsigned)blocks), dim3(kThreads), 0,
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, BF16>), dim3((unsigned)blocks), dim3(kThreads), 0,
                      st, p);
   if (pl.slab_elems)
     hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.tail_cols)), dim3(256), 0, st, slab, pl.S,
@@ -908,15 +1162,42 @@ hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t 
   return hipGetLastError();
 }
 
-template <int MODE, bool BSCALE>
+template <int TM, int MODE, bool BSCALE>
+hipError_t launch_direct(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t st) {
+  constexpr int BN = 4 * 32 * kDirectTN;
+  p.gy = pl.gy;
+  p.nfull_t = pl.nfull_t;
+  p.full_blocks = pl.nfull_t * pl.gy;
+  p.S = pl.S;
+  p.kt_per_split = pl.kt_per_split;
+  p.tail_n0 = pl.nfull_t * BN;
+  p.tail_cols = std::max(0, p.N - p.tail_n0);
+  p.slab = pl.slab_elems ? slab : nullptr;
+  const long blocks = (long)p.full_blocks + (long)(pl.gx - pl.nfull_t) * pl.gy * pl.S;
+  hipLaunchKernelGGL((conv_direct_kernel<TM, kDirectTN, MODE, BSCALE>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
+                     p);
+  if (pl.slab_elems)
+    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.tail_cols)), dim3(256), 0, st, slab, pl.S,
+                       p.M, p.tail_cols, p.tail_n0, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
+                       p.y);
+  return hipGetLastError();
+}
+
+template <int MODE, bool BSCALE, bool BF16>
 hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab, hipStream_t st) {
-  if (pl.bm == 128 && pl.bn == 256) return launch_conv<128, 256, 2, 2, MODE, BSCALE>(p, pl, slab, st);
-  if (pl.bm == 256 && pl.bn == 128) return launch_conv<256, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
+  if (conv_direct() && !BF16) {
+    switch (pl.bm) {
+      case 32: return launch_direct<1, MODE, BSCALE>(p, pl, slab, st);
+      case 64: return launch_direct<2, MODE, BSCALE>(p, pl, slab, st);
+      case 96: return launch_direct<3, MODE, BSCALE>(p, pl, slab, st);
+      default: return launch_direct<4, MODE, BSCALE>(p, pl, slab, st);
+    }
+  }
   switch (pl.bm) {
-    case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE>(p, pl, slab, st);
-    case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
-    case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE>(p, pl, slab, st);
-    default: return launch_conv<128, 128, 2, 2, MODE, BSCALE>(p, pl, slab, st);
+    case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
+    case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
+    case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
+    default: return launch_conv<128, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
   }
 }
 
@@ -925,10 +1206,25 @@ void launch_pack(const ConvArgs& p, int mpad, int ckp, float* packed, hipStream_
                      p.M, p.Ck, p.T, mpad, ckp, packed);
 }
 
+template <bool BF16>
+hipError_t dispatch_conv_mode(const ConvArgs& p, const ConvPlan& pl, float* slab, hipStream_t st, bool s) {
+  switch (p.g.mode) {
+    case kZero:
+      return s ? dispatch_conv_tile<kZero, true, BF16>(p, pl, slab, st)
+               : dispatch_conv_tile<kZero, false, BF16>(p, pl, slab, st);
+    case kReplicate:
+      return s ? dispatch_conv_tile<kReplicate, true, BF16>(p, pl, slab, st)
+               : dispatch_conv_tile<kReplicate, false, BF16>(p, pl, slab, st);
+    default:
+      return s ? dispatch_conv_tile<kTransposed, true, BF16>(p, pl, slab, st)
+               : dispatch_conv_tile<kTransposed, false, BF16>(p, pl, slab, st);
+  }
+}
+
 // p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
 // GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
-  const ConvPlan pl = conv_plan(p.M, p.N, p.Ck, p.T, p.g.mode, p.g.scale != nullptr);
+  const ConvPlan pl = conv_plan(p.M, p.N, p.Ck, p.T, p.g.mode, p.g.scale != nullptr, p.bf16 != 0);
   if ((pl.slab_elems && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
   const int mpad = (p.M + pl.bm - 1) / pl.bm * pl.bm;
   p.Ckp = (p.Ck + BK - 1) / BK * BK;
@@ -938,25 +1234,16 @@ hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab,
   }
   p.w_bytes = 4 * mpad * p.T * p.Ckp;
   const bool s = p.g.scale != nullptr;
-  switch (p.g.mode) {
-    case kZero:
-      return s ? dispatch_conv_tile<kZero, true>(p, pl, slab, st) : dispatch_conv_tile<kZero, false>(p, pl, slab, st);
-    case kReplicate:
-      return s ? dispatch_conv_tile<kReplicate, true>(p, pl, slab, st)
-               : dispatch_conv_tile<kReplicate, false>(p, pl, slab, st);
-    default:
-      return s ? dispatch_conv_tile<kTransposed, true>(p, pl, slab, st)
-               : dispatch_conv_tile<kTransposed, false>(p, pl, slab, st);
-  }
+  return p.bf16 ? dispatch_conv_mode<true>(p, pl, slab, st, s) : dispatch_conv_mode<false>(p, pl, slab, st, s);
 }
 
-template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED>
+template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED, bool BF16>
 hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStream_t st) {
   const int gx = (p.J + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
   p.kt_per_split = pl.kt_per_split;
   p.splits = pl.splits;
   p.slab = pl.splits > 1 ? slab : nullptr;
-  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED>), dim3(gx, gy, T * pl.splits), dim3(kThreads),
+  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED, BF16>), dim3(gx, gy, T * pl.splits), dim3(kThreads),
                      0, st, p);
   if (pl.splits > 1)
     hipLaunchKernelGGL(wgrad_split_reduce_kernel, dim3(grid1d(p.out_numel)), dim3(256), 0, st, slab, pl.splits,
@@ -964,14 +1251,14 @@ hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStre
   return hipGetLastError();
 }
 
-template <int MODE, bool SCALED>
+template <int MODE, bool SCALED, bool BF16>
 hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, const Plan& pl, float* slab, hipStream_t st) {
-  if (pl.bn == 64) return launch_wgrad<64, 64, 2, 2, MODE, SCALED>(p, T, pl, slab, st);
+  if (pl.bn == 64) return launch_wgrad<64, 64, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
   switch (pl.bm) {
-    case 32: return launch_wgrad<32, 128, 1, 4, MODE, SCALED>(p, T, pl, slab, st);
-    case 64: return launch_wgrad<64, 128, 2, 2, MODE, SCALED>(p, T, pl, slab, st);
-    case 96: return launch_wgrad<96, 128, 1, 4, MODE, SCALED>(p, T, pl, slab, st);
-    default: return launch_wgrad<128, 128, 2, 2, MODE, SCALED>(p, T, pl, slab, st);
+    case 32: return launch_wgrad<32, 128, 1, 4, MODE, SCALED, BF16>(p, T, pl, slab, st);
+    case 64: return launch_wgrad<64, 128, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
+    case 96: return launch_wgrad<96, 128, 1, 4, MODE, SCALED, BF16>(p, T, pl, slab, st);
+    default: return launch_wgrad<128, 128, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
   }
 }
 
@@ -980,16 +1267,24 @@ hipError_t dispatch_wgrad(const WgradArgs& p, int T, float* slab, hipStream_t st
   if (s && !(p.ascale && p.g.scale)) return hipErrorInvalidValue;  // both scales or none
   const Plan pl = wgrad_plan(p.M, p.J, p.K, T, s);
   if (pl.splits > 1 && !slab) return hipErrorInvalidValue;
+  if (p.bf16) {
+    if (p.g.mode == kReplicate)
+      return s ? dispatch_wgrad_tile<kReplicate, true, true>(p, T, pl, slab, st)
+               : dispatch_wgrad_tile<kReplicate, false, true>(p, T, pl, slab, st);
+    return s ? dispatch_wgrad_tile<kZero, true, true>(p, T, pl, slab, st)
+             : dispatch_wgrad_tile<kZero, false, true>(p, T, pl, slab, st);
+  }
   if (p.g.mode == kReplicate)
-    return s ? dispatch_wgrad_tile<kReplicate, true>(p, T, pl, slab, st)
-             : dispatch_wgrad_tile<kReplicate, false>(p, T, pl, slab, st);
-  return s ? dispatch_wgrad_tile<kZero, true>(p, T, pl, slab, st)
-           : dispatch_wgrad_tile<kZero, false>(p, T, pl, slab, st);
+    return s ? dispatch_wgrad_tile<kReplicate, true, false>(p, T, pl, slab, st)
+             : dispatch_wgrad_tile<kReplicate, false, false>(p, T, pl, slab, st);
+  return s ? dispatch_wgrad_tile<kZero, true, false>(p, T, pl, slab, st)
+           : dispatch_wgrad_tile<kZero, false, false>(p, T, pl, slab, st);
 }
 
 bool desc_ok(const ganamd_conv_desc* d) {
   return d && d->B > 0 && d->Cin > 0 && d->Cout > 0 && d->H > 0 && d->W > 0 && d->OH > 0 && d->OW > 0 &&
-         d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0;
+         d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0 &&
+         (d->math == GANAMD_MATH_F32 || d->math == GANAMD_MATH_BF16);
 }
 
 }  // namespace
@@ -1076,8 +1371,8 @@ static int fwd_mode(const ganamd_conv_desc* d) {
   return d->transposed ? kTransposed : (d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero);
 }
 static int dgrad_mode(const ganamd_conv_desc* d) { return (dgrad_scatter(d) || d->transposed) ? kZero : kTransposed; }
-static size_t slab_bytes(int M, int N, int Ck, int T, int mode) {
-  const long a = conv_plan(M, N, Ck, T, mode, false).slab_elems, b = conv_plan(M, N, Ck, T, mode, true).slab_elems;
+static size_t slab_bytes(int M, int N, int Ck, int T, int mode, bool bf16) {
+  const long a = conv_plan(M, N, Ck, T, mode, false, bf16).slab_elems, b = conv_plan(M, N, Ck, T, mode, true, bf16).slab_elems;
   return sizeof(float) * (size_t)std::max(a, b);
 }
 
@@ -1097,9 +1392,10 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
   else
     dgrad_gemm(d, &M, &N, &Ck, &T);
   const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
-  const ConvPlan pl = conv_plan(M, N, Ck, T, mode, scaled != 0);
+  const ConvPlan pl = conv_plan(M, N, Ck, T, mode, scaled != 0, d->math == GANAMD_MATH_BF16);
   const int v[10] = {pl.bm, pl.bn, pl.gx, pl.gy, pl.nfull_t, pl.S, pl.kt_per_split,
-                     pl.nfull_t * pl.gy + (pl.gx - pl.nfull_t) * pl.gy * pl.S, conv_occupancy(pl.bm, pl.bn, mode, scaled),
+                     pl.nfull_t * pl.gy + (pl.gx - pl.nfull_t) * pl.gy * pl.S,
+                     conv_occupancy(pl.bm, pl.bn, mode, scaled, d->math == GANAMD_MATH_BF16),
                      num_cus()};
   for (int i = 0; i < 10; ++i) info[i] = v[i];
   return GANAMD_OK;
@@ -1147,11 +1443,11 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   *bytes = 0;
   if (op == GANAMD_CONV_FWD) {
     fwd_gemm(d, &M, &N, &Ck, &T);
-    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + slab_bytes(M, N, Ck, T, fwd_mode(d));
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + slab_bytes(M, N, Ck, T, fwd_mode(d), d->math == GANAMD_MATH_BF16);
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
-             align256(dgrad_scatter_bytes(d)) + slab_bytes(M, N, Ck, T, dgrad_mode(d));
+             align256(dgrad_scatter_bytes(d)) + slab_bytes(M, N, Ck, T, dgrad_mode(d), d->math == GANAMD_MATH_BF16);
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
     T = d->KH * d->KW;
@@ -1202,6 +1498,7 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   p.alpha = alpha;
   p.N = N;
   p.ohw = d->OH * d->OW;
+  p.bf16 = d->math == GANAMD_MATH_BF16;
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
   float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))));
@@ -1229,6 +1526,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   p.oscale = nullptr;
   p.alpha = alpha;
   p.N = N;
+  p.bf16 = d->math == GANAMD_MATH_BF16;
   const size_t pad_bytes = dgrad_pad_bytes(d);
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
@@ -1278,6 +1576,7 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
   WgradArgs p{};
   p.alpha = alpha;
   p.ot = 1;
+  p.bf16 = d->math == GANAMD_MATH_BF16;
   if (d->transposed) {
     // dW[ci][co][t] = sum_n x[ci][n] * gy[co][conv-gather_t(n)]
     p.a = x;

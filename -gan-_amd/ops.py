@@ -13,6 +13,8 @@ Generator-only operators (fused BatchNorm+PReLU, the modulated conv) are first-o
 """
 from __future__ import annotations
 
+import contextlib
+
 from dataclasses import dataclass
 
 import torch
@@ -44,16 +46,16 @@ class Geo:
     transposed: bool = False
 
     def desc(self, packed=False):
-        key = (self, packed)
+        key = (self, packed, _MATH[0])
         d = _DESC_CACHE.get(key)
         if d is None:
             d = _lib.ConvDesc(self.B, self.Cin, self.H, self.W, self.Cout, self.OH, self.OW, self.K, self.K,
-                              self.stride, self.pad, self.pad_mode, int(self.transposed), int(packed))
+                              self.stride, self.pad, self.pad_mode, int(self.transposed), int(packed), _MATH[0])
             _DESC_CACHE[key] = d
         return d
 
     def ws_bytes(self, op, packed=False):
-        key = (self, op, packed)
+        key = (self, op, packed, _MATH[0])
         v = _WS_CACHE.get(key)
         if v is None:
             n = _lib.c_size_t(0)
@@ -68,6 +70,20 @@ class Geo:
 
 _DESC_CACHE: dict = {}
 _WS_CACHE: dict = {}
+_MATH = [_lib.MATH_F32]      # arithmetic of the conv GEMMs launched now (math_mode)
+
+
+@contextlib.contextmanager
+def math_mode(mode: str):
+    """Run the conv / linear GEMMs issued inside the block in ``"fp32"`` (exact fp32 MFMA, the
+    default) or ``"bf16"`` (operands rounded to bf16, fp32 accumulation and storage).  Applies to
+    the launches made while the block is active -- wrap the backward too."""
+    prev = _MATH[0]
+    _MATH[0] = {"fp32": _lib.MATH_F32, "bf16": _lib.MATH_BF16}[mode]
+    try:
+        yield
+    finally:
+        _MATH[0] = prev
 
 
 PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus")

@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import torch
 
-from . import wgangp
+from . import ops, wgangp
 from .optim import FusedAdamW
 
 LAZY_INTERVAL = 5      # wganlazygpR2.py:56,65,71: regularisers every 5th critic step
@@ -34,6 +34,18 @@ GP_LAMBDA = 10         # :72
 
 
 class Train(wgangp.Train):
+    """``precision="bf16"`` (config 4 of BASELINE.json: "bf16 with fp32 GP"): the plain critic
+    steps and the generator steps run their conv / linear GEMMs with bf16 operands (fp32
+    accumulation, fp32 activations, weights, gradients and optimizer state); the regularised
+    critic steps -- R1, R2 and the gradient penalty with their double backward -- stay fp32.
+    The reference has no mixed precision: the bf16 path is checked against the
+    fp32 fixtures at a documented looser tolerance (tests/test_models_gpu.py)."""
+
+    def __init__(self, *args, precision: str = "fp32", **kw):
+        assert precision in ("fp32", "bf16"), precision
+        self.precision = precision
+        super().__init__(*args, **kw)
+
     def make_optimizers(self):
         """trainunits.py:18-19: torch.optim.Adam (weight_decay 0)."""
         return (FusedAdamW(self.generator, lr=0.0001, betas=(0.5, 0.99), weight_decay=0.0),
@@ -45,17 +57,23 @@ class Train(wgangp.Train):
         self.optimizer_D.step()
         return out
 
+    def generator_backward(self, b_size):
+        with ops.math_mode(self.precision):
+            return super().generator_backward(b_size)
+
     def discriminator_backward(self, images, b_size, idx):
         self.optimizer_D.zero_grad()
         z = self.rng.randn((b_size, self.nz, 1, 1))
-        with torch.no_grad():
+        plain = idx % LAZY_INTERVAL != 0
+        with ops.math_mode(self.precision if plain else "fp32"), torch.no_grad():
             gen_imgs = self._generate(z)
         images = images.detach()
-        if idx % LAZY_INTERVAL != 0:
-            pred = self.discriminator(torch.cat([images, gen_imgs]), segments=2)
-            real_loss = -torch.mean(pred[:b_size])
-            fake_loss = torch.mean(pred[b_size:])
-            (real_loss + fake_loss).backward()
+        if plain:
+            with ops.math_mode(self.precision):
+                pred = self.discriminator(torch.cat([images, gen_imgs]), segments=2)
+                real_loss = -torch.mean(pred[:b_size])
+                fake_loss = torch.mean(pred[b_size:])
+                (real_loss + fake_loss).backward()
             zero = torch.zeros(1, device=images.device)
             return real_loss, fake_loss, zero, zero.clone(), zero.clone()
         eps = self.rng.rand((b_size,)).view(b_size, 1, 1, 1)

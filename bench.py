@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--config", choices=["wgangp", "lazy", "progan"], default="wgangp",
                     help="wgangp = the headline (configs 2/3); lazy = config 4 (fp32); progan = config 5")
     ap.add_argument("--mode", choices=["eager", "graph"], default="graph")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
+                    help="GEMM arithmetic (lazy config only; default bf16 there, as config 4 specifies)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-extras", action="store_true",
@@ -145,7 +147,7 @@ CONFIGS = {
     "wgangp": (METRIC, 64, "G13_5+D9_4 WGAN-GP iteration (5 critic steps with GP + 1 generator step), 64x64x3"),
     "lazy": ("images/sec per lazy-GP+R1/R2 period (G13_5+D9_4, 64x64, wganlazygpR2, 5 batches)", 128,
              "G13_5+D9_4 train/wganlazygpR2.py: 5 batches = 5 x (critic step + generator step), R1/R2/GP on the "
-             "first, Adam; config 4 of BASELINE.json (fp32 here)"),
+             "first, Adam; config 4 of BASELINE.json"),
     "progan": ("images/sec per WGAN-GP iter (generator_3_progan ngf=256 + discriminator_3_wgangp_progan ndf=64, "
                "64x64, n_critic=5)", 64,
                "progan pair under train/wgangp.py, fixed 64x64 nets (the reference has no progressive schedule); "
@@ -166,8 +168,11 @@ def build(args, dev, rank):
         G.use_bank = not args.no_bank
         D = gan_amd.Discriminator().to(dev)
     torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
-    Tr = gan_amd.wganlazygpR2.Train if args.config == "lazy" else gan_amd.Train
-    tr = Tr([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev))
+    if args.config == "lazy":
+        tr = gan_amd.wganlazygpR2.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev),
+                                        precision=args.precision)
+    else:
+        tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev))
     B = args.batch
 
     def real():
@@ -189,6 +194,10 @@ def main():
     args = parse()
     if args.batch is None:
         args.batch = CONFIGS[args.config][1]
+    if args.precision is None:
+        args.precision = "bf16" if args.config == "lazy" else "fp32"
+    if args.precision == "bf16" and args.config != "lazy":
+        raise SystemExit("--precision bf16 applies to --config lazy (config 4); the headline is fp32")
     world, rank, local = setup_dist(args.gpus, args.backend)
     dev = torch.device("cuda", torch.cuda.current_device())
     from gan_amd import ops
@@ -315,7 +324,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.precision == "fp32" else "bf16 GEMM operands, fp32 accumulate/storage; fp32 R1/R2/GP steps",
             "data": "synthetic N(0,1) real batches drawn on device each critic step; random reference-init weights",
             "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
                        "parallelism": f"dp{world}", "mode": args.mode},

@@ -35,6 +35,11 @@ extern "C" {
 #define GANAMD_PAD_ZERO 0
 #define GANAMD_PAD_REPLICATE 1
 
+/* Arithmetic of the conv GEMMs: fp32 MFMA (exact fp32 products, the default), or operands
+ * rounded to bf16 (RNE) with fp32 accumulation and fp32 storage (the bf16 configuration). */
+#define GANAMD_MATH_F32 0
+#define GANAMD_MATH_BF16 1
+
 #define GANAMD_CONV_FWD 0
 #define GANAMD_CONV_DGRAD 1
 #define GANAMD_CONV_WGRAD 2
@@ -51,6 +56,7 @@ typedef struct ganamd_conv_desc {
   int32_t transposed;
   int32_t packed_w;   /* 1: the w argument of conv_fwd/conv_dgrad is already in GEMM order
                          (ganamd_conv_pack for the same op and geometry); 0: as stored */
+  int32_t math;       /* GANAMD_MATH_F32 | GANAMD_MATH_BF16 */
 } ganamd_conv_desc;
 
 /* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD). */

@@ -41,7 +41,7 @@ def test_library_is_gfx950():
 def test_invalid_arguments_rejected():
     from gan_amd import _lib
     L = _lib.LIB
-    d = _lib.ConvDesc(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)   # B = 0: invalid geometry
+    d = _lib.ConvDesc(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)   # B = 0: invalid geometry
     n = _lib.c_size_t(0)
     assert L.ganamd_conv_workspace(d, 0, n) == -1
     assert L.ganamd_conv_fwd(d, None, None, None, None, None, 1.0, None, None, None) == -1
@@ -52,11 +52,13 @@ def test_invalid_arguments_rejected():
 def test_workspace_sizes():
     from gan_amd import _lib
     L = _lib.LIB
-    d = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0)
+    d = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 0)
     n = _lib.c_size_t(0)
     assert L.ganamd_conv_workspace(d, _lib.CONV_DGRAD, n) == 0
     assert n.value >= 4 * 8 * 4 * 18 * 18
     assert L.ganamd_rowreduce_workspace(8, 4096) >= 8 * 3 * 4
+    bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 7)      # unknown math mode
+    assert L.ganamd_conv_workspace(bad, _lib.CONV_FWD, n) == -1
 
 
 @pytest.mark.parametrize("bad", ["x", "w"])

@@ -293,3 +293,42 @@ def test_progan_steps(gan):
     assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-4
     check_vs_truth(_rows(G, [n for n, _, _ in pp["g_params"]]), t64["g_grads"], t64["ref_g_stats"],
                    t64["g_fp32_spread"])
+
+
+# ---- bf16 configuration (config 4: "bf16 with fp32 GP") ---------------------------------------
+
+def test_lazy_bf16_steps(gan, P):
+    """precision="bf16": a plain critic step and a generator step with bf16 GEMM operands against
+    the reference's fp32 fixture at a bf16 bar (the reference has no bf16), and
+    the regularised step (R1/R2/GP) bit-identical to the fp32 trainer's (it stays fp32)."""
+    fx = fixture("lazy_b4.npz")
+    # plain critic step (idx 1): losses within 2e-2 of fp32, and measurably not fp32
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(511, DEV),
+                                precision="bf16")
+    images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(510)).to(DEV)
+    losses = [float(v.detach().reshape(-1)[0]) for v in tr.discriminator_trainstep(images, 4, 1)]
+    er = rel_err(losses[:1], fx["d1_losses"][:1])
+    ef = rel_err(losses[1:2], fx["d1_losses"][1:2])
+    print("bf16 critic losses", losses[:2], "fp32 reference", list(fx["d1_losses"][:2]), "rel", er, ef)
+    # the real loss is the critic alone (19 bf16 conv blocks): measured 3e-4; the fake loss also
+    # carries G13_5's output, whose ~100 sequential layers with BatchNorm1d over B=4 amplify
+    # rounding ~10^3-fold (fp32 alone: 2e-4 from float64, test_reference_fp32_error): measured 3.6e-2
+    assert 1e-6 < er < 2e-3 and 1e-6 < ef < 8e-2
+    # generator step: loss within 2e-2; Adam's first update ~ lr*sign(g) per element
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(601, DEV),
+                                precision="bf16")
+    _gen, g_loss = tr.generator_trainstep(4)
+    err = rel_err([float(g_loss.detach())], fx["g_loss"])
+    print("bf16 generator loss", float(g_loss), "fp32 reference", float(fx["g_loss"][0]), "rel", err)
+    assert 1e-6 < err < 8e-2        # G13_5 output through the critic, as the fake loss above
+    # the regularised step stays fp32: identical to the fp32 trainer on the same inputs
+    out = []
+    for prec in ("fp32", "bf16"):
+        G, D = make_G(gan, P), make_D(gan, P)
+        tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(601, DEV),
+                                    precision=prec)
+        images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(600)).to(DEV)
+        out.append([float(v.detach().reshape(-1)[0]) for v in tr.discriminator_trainstep(images, 4, 0)])
+    assert out[0] == out[1], out

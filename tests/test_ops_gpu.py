@@ -535,3 +535,27 @@ def test_conv_tail_split_schedule(ops, case):
     assert rel(got.permute(1, 0, 2, 3), gx) < 2e-5
     # at least the fwd or dgrad plan of each case exercises the mixed schedule on MI355X
     assert any(0 < q["nfull_t"] < q["gx"] and q["S"] > 1 for q in (pf, pd)), (pf, pd)
+
+
+@pytest.mark.parametrize("case", [(4, 48, 16, 48, 5, 1, 2, 1), (4, 64, 8, 200, 3, 1, 1, 1), (4, 16, 8, 33, 3, 2, 1, 1),
+                                  (4, 1025, 4, 1025, 3, 1, 1, 1)])
+def test_conv_bf16_math(ops, case):
+    """GANAMD_MATH_BF16: operands rounded to bf16, fp32 accumulation -- fwd / dgrad / wgrad within
+    a bf16 bar (2^-8 relative per operand) of float64, and measurably different from fp32."""
+    B, Cin, H, Cout, k, s, p, mode = case
+    g = torch.Generator().manual_seed(sum(case) + 1)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64, requires_grad=True)
+    y = ref_conv(x, w * 0.3, None, k, s, p, mode)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    gx, gw = torch.autograd.grad(y, (x, w), gy)
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, s, p, mode)
+    xg, wg, gyg = cn(x), w.detach().float().to(DEV), cn(gy)
+    got = {}
+    for m in ("fp32", "bf16"):
+        with ops.math_mode(m):
+            got[m] = (nc(ops._conv_fwd(geo, xg, wg, alpha=0.3)), nc(ops._conv_dgrad(geo, gyg, wg, alpha=0.3)),
+                      ops._conv_wgrad(geo, xg, gyg, alpha=0.3))
+    for ref, a32, a16 in zip((y, gx, gw), got["fp32"], got["bf16"]):
+        e32, e16 = rel(a32, ref), rel(a16, ref)
+        assert e32 < 1e-5 and 3e-4 < e16 < 1e-2, (e32, e16)
