@@ -547,12 +547,46 @@ class GeneratorStart(nn.Module):
 
 
 class _NoiseHub:
-    """Where StyleConv gets its N(0,1) noise; a Generator-wide hook so callers can replay draws."""
+    """Where StyleConv gets its N(0,1) noise; a Generator-wide hook so callers can replay draws.
+
+    A forward makes 253 noise draws (generator_13_5.py:265).  When the source can draw in bulk
+    (DeviceRNG.noise_bulk) and a previous forward at the same batch recorded the draw shapes,
+    the hub draws ALL of a forward's noise with one launch at its start and hands out views in
+    the same order (one launch instead of 253; inside a captured graph the bulk draw is captured
+    too, so every replay gets fresh noise).  A replaying source (ReplayRNG) keeps the per-draw
+    path and the reference's draw order."""
 
     def __init__(self):
         self.source = None
+        self.bulk_source = None     # numel -> flat N(0,1) tensor, or None (per-draw only)
+        self.shapes = {}            # batch -> the draw shapes of one forward
+        self._rec = None
+        self._bulk = None
+
+    def begin(self, batch):
+        self._rec, self._bulk = [], None
+        bulk = self.bulk_source if self.source is not None else None
+        shapes = self.shapes.get(batch)
+        if bulk is not None and shapes:
+            total = sum(C * B * H * W for B, C, H, W in shapes)
+            self._bulk = (bulk(total), list(shapes), 0, 0)
+
+    def end(self, batch):
+        if self._rec is not None:
+            self.shapes[batch] = self._rec
+        self._rec, self._bulk = None, None
 
     def noise(self, shape_nchw):
+        if self._rec is not None:
+            self._rec.append(tuple(shape_nchw))
+        if self._bulk is not None:
+            buf, shapes, i, off = self._bulk
+            if i < len(shapes) and shapes[i] == tuple(shape_nchw):
+                B, C, H, W = shape_nchw
+                n = C * B * H * W
+                self._bulk = (buf, shapes, i + 1, off + n)
+                return buf[off:off + n].view(C, B, H, W)
+            self._bulk = None           # the draw sequence changed: per-draw from here on
         if self.source is not None:
             return self.source(shape_nchw)
         B, C, H, W = shape_nchw
@@ -622,6 +656,7 @@ class Generator(nn.Module):
             raise NotImplementedError("G13_5 is only ever run in train mode (batch statistics)")
         bank = self._bank()
         self.block0.__dict__["_w_hook"] = self._run_bank if bank is not None else None
+        self.noise_hub.begin(x.shape[0])
         try:
             h, w, rgb = self.block0(x)
             h, rgb = self.block1(h, w, rgb)
@@ -629,6 +664,7 @@ class Generator(nn.Module):
             h, rgb = self.block3(h, w, rgb)
             h, rgb = self.block4(h, w, rgb)
         finally:
+            self.noise_hub.end(x.shape[0])
             if bank is not None:
                 for m in bank.mods:
                     m.__dict__["_bank_sd"] = None

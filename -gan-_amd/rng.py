@@ -26,6 +26,10 @@ class DeviceRNG:
         B, C, H, W = shape_nchw
         return torch.randn((C, B, H, W), device=self.device)
 
+    def noise_bulk(self, numel):
+        """All of one generator forward's noise in one draw (generator_13_5._NoiseHub)."""
+        return torch.randn(numel, device=self.device)
+
 
 class ReplayRNG:
     """Draws from one CPU generator in call order, returns device tensors (CNHW for noise)."""

@@ -67,6 +67,7 @@ class Train(CheckpointMixin):
         hub = getattr(self.generator, "noise_hub", None)      # G13_5's in-forward noise (progan has none)
         if hub is not None:
             hub.source = self.rng.noise
+            hub.bulk_source = getattr(self.rng, "noise_bulk", None)   # DeviceRNG: one draw per forward
         return self.generator(z)
 
     def generator_trainstep(self, b_size):
@@ -111,12 +112,21 @@ class Train(CheckpointMixin):
         self.optimizer_D.step()
         return out
 
-    def discriminator_backward(self, images, b_size):
-        """discriminator_trainstep up to (not including) the optimizer step."""
-        self.optimizer_D.zero_grad()
+    def generate_fake(self, b_size):
+        """The critic step's fake batch (wgangp.py:58-59): z draw, then G under no_grad.  It
+        depends on the generator's weights only, so a data-parallel driver may compute the NEXT
+        critic step's batch on a second stream while this step's gradient all-reduce and
+        optimizer update run (bench.py)."""
         z = self.rng.randn((b_size, self.nz, 1, 1))
         with torch.no_grad():
-            gen_imgs = self._generate(z)
+            return self._generate(z)
+
+    def discriminator_backward(self, images, b_size, gen_imgs=None):
+        """discriminator_trainstep up to (not including) the optimizer step.  ``gen_imgs``: a fake
+        batch made beforehand by generate_fake (default: made here, in the reference's order)."""
+        self.optimizer_D.zero_grad()
+        if gen_imgs is None:
+            gen_imgs = self.generate_fake(b_size)
         gen_imgs.requires_grad_()
         # The real and fake batches go through the critic as ONE pass of 2B samples (two
         # MiniBatchStdDev segments, see Discriminator.forward): the critic is per-sample apart

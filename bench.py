@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
     ap.add_argument("--config", choices=["wgangp", "lazy", "progan"], default="wgangp",
-                    help="wgangp = the headline (configs 2/3); lazy = config 4 (fp32); progan = config 5")
+                    help="wgangp = the headline (configs 2/3); lazy = config 4 (bf16 GEMMs, fp32 R1/R2/GP); progan = config 5")
     ap.add_argument("--mode", choices=["eager", "graph"], default="graph")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="GEMM arithmetic (lazy config only; default bf16 there, as config 4 specifies)")
@@ -56,6 +56,8 @@ def parse():
                     help="skip the post-run breakdown and roofline probe (clean traces of the timed region)")
     ap.add_argument("--no-bank", action="store_true", help="per-module style MLPs (A/B against the style bank)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: no second-stream fake-batch generation during the critic all-reduce (A/B)")
     return ap.parse_args()
 
 
@@ -101,11 +103,13 @@ def cpu_baseline(threads):
                       f"{t2 - t1:.2f}s, t_iter = 5*t_D + t_G = {t_iter:.1f}s; nproc={os.cpu_count()}"}
 
 
-# Dominant kernel: the implicit-GEMM conv kernel (conv_gemm_kernel, all instances ~55 % of the
-# iteration's GPU time; profiles/).  Representative launch: the critic's mid-level block conv in
-# the real+fake pass -- D9_4 128->128 channels, 3x3 replication pad, 32x32, B = 128 -- one
-# conv_gemm_kernel<128,128,2,2,1,false> launch per call (1024 tiles, no split-K).
-PROBE = dict(B=128, cin=128, h=32, cout=128, k=3)
+# Dominant kernel: the implicit-GEMM conv kernel (conv_gemm_kernel, all instances ~55-65 % of the
+# iteration's GPU time; profiles/).  Representative launch: the critic's mid-level block conv --
+# D9_4 128->128 channels, 3x3 replication pad, 32x32 -- at B = 96: 768 output tiles = exactly one
+# round of the kernel's 3 resident blocks per CU, so the block schedule (ConvPlan) keeps whole
+# tiles and the call is ONE conv_gemm_kernel<128,128,2,2,1,false,false> launch (at the critic's
+# B = 128 it would add K-split tail blocks and a reduce launch).
+PROBE = dict(B=96, cin=128, h=32, cout=128, k=3)
 
 
 def roofline_probe(dev, reps=20):
@@ -113,6 +117,8 @@ def roofline_probe(dev, reps=20):
     g = ops.conv_geo(PROBE["B"], PROBE["cin"], PROBE["h"], PROBE["h"], PROBE["cout"], PROBE["k"], 1, 1)
     x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
     w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
+    pl = ops.plan_info(g, 0, False)
+    assert pl["nfull_t"] == pl["gx"] and pl["S"] == 1, pl      # one launch, whole tiles
     with torch.no_grad():
         for _ in range(3):
             ops._conv_fwd(g, x, w, None, None, None, 0.03)   # packs the weight once (ops.PackCache)
@@ -128,8 +134,8 @@ def roofline_probe(dev, reps=20):
     us = e0.elapsed_time(e1) * 1e3 / reps
     flop = 2.0 * g.B * g.OH * g.OW * g.Cout * g.Cin * g.K * g.K
     tf = flop / us / 1e6
-    out = {"bound": "mfma", "kernel": "conv_gemm_kernel<128,128,2,2,1,false>",
-           "shape": "conv fwd B=128 128->128 3x3 replicate-pad 32x32 (D9_4 block conv, critic real+fake pass)",
+    out = {"bound": "mfma", "kernel": "conv_gemm_kernel<128,128,2,2,1,false,false>",
+           "shape": "conv fwd B=96 128->128 3x3 replicate-pad 32x32 (D9_4 block conv; 768 whole tiles, one launch)",
            "algorithmic_gflop_per_launch": flop / 1e9, "launch_us": us,
            "achieved": tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP32_MFMA_PEAK_TFLOPS,
            "traffic": None}
@@ -243,35 +249,76 @@ def main():
         pool = torch.cuda.graph_pool_handle()
         torch.cuda.empty_cache()
 
-        def capture(fn):
+        def capture(fn, gpool=None):
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 fn()
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool if gpool is None else gpool):
                 fn()
             return g
 
-        for key, bwd, opt, _ in phases:
-            if key in graphs:
-                continue
-            if world == 1:
-                graphs[key] = (capture(lambda b=bwd, o=opt: (b(), o.step())), None, opt)
-            else:
-                graphs[key] = (capture(bwd), capture(opt.step), opt)
-        torch.cuda.synchronize()
-        if rank == 0:
-            print(f"[bench] captured {len(graphs)} phase graphs", file=sys.stderr, flush=True)
+        if world > 1 and args.config == "wgangp" and not args.no_overlap:
+            # Data-parallel critic steps with the overlap SURVEY.md §8(e)(2) allows: the next
+            # critic step's fake batch (no-grad G forward, 41 % of a critic step's FLOPs) depends
+            # on G's weights only, so it runs on a second stream while this step's RCCL
+            # all-reduce of the critic gradient and the AdamW update run on the main stream.
+            # The fake-batch graph has its own memory pool (it replays concurrently with others).
+            fake = {}
 
-        def step():
-            for key, *_ in phases:
-                gb, go, opt = graphs[key]
-                gb.replay()
-                if go is not None:
-                    allreduce_mean_(opt.flat.grad)
-                    go.replay()
+            def gfwd():
+                fake["x"] = tr.generate_fake(B)
+
+            g_fwd = capture(gfwd, torch.cuda.graph_pool_handle())
+            g_fwd.replay()                       # a valid fake batch for the captures below
+            g_crit = capture(lambda: tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B,
+                                                               gen_imgs=fake["x"]))
+            g_dstep = capture(tr.optimizer_D.step)
+            g_gen = capture(lambda: tr.generator_backward(B))
+            g_gstep = capture(tr.optimizer_G.step)
+            graphs = {"fake": (g_fwd, None, None), "critic": (g_crit, g_dstep, tr.optimizer_D),
+                      "gen": (g_gen, g_gstep, tr.optimizer_G)}
+            side = torch.cuda.Stream()
+            torch.cuda.synchronize()
+            if rank == 0:
+                print("[bench] captured the pipelined data-parallel graphs", file=sys.stderr, flush=True)
+
+            def step():
+                cur = torch.cuda.current_stream()
+                g_fwd.replay()                   # G changed in the previous generator step
+                for i in range(N_CRITIC):
+                    g_crit.replay()
+                    if i + 1 < N_CRITIC:
+                        side.wait_stream(cur)    # this step's critic has read the fake batch
+                        with torch.cuda.stream(side):
+                            g_fwd.replay()
+                    allreduce_mean_(tr.optimizer_D.flat.grad)
+                    g_dstep.replay()
+                    cur.wait_stream(side)
+                g_gen.replay()
+                allreduce_mean_(tr.optimizer_G.flat.grad)
+                g_gstep.replay()
+        else:
+            for key, bwd, opt, _ in phases:
+                if key in graphs:
+                    continue
+                if world == 1:
+                    graphs[key] = (capture(lambda b=bwd, o=opt: (b(), o.step())), None, opt)
+                else:
+                    graphs[key] = (capture(bwd), capture(opt.step), opt)
+            torch.cuda.synchronize()
+            if rank == 0:
+                print(f"[bench] captured {len(graphs)} phase graphs", file=sys.stderr, flush=True)
+
+            def step():
+                for key, *_ in phases:
+                    gb, go, opt = graphs[key]
+                    gb.replay()
+                    if go is not None:
+                        allreduce_mean_(opt.flat.grad)
+                        go.replay()
 
     if world > 1:
         dist.barrier()
