@@ -655,6 +655,9 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
+  // Block order: consecutive blocks are consecutive K-slices of one tap (they stream adjacent
+  // pixel ranges of gy and x).  A tap-fastest order with an XCD-contiguous remap, meant to share
+  // the taps' overlapping source rows through one XCD's L2, measured 5-15 % slower.
   const int j0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int t = blockIdx.z / p.splits;
   const int split = blockIdx.z - t * p.splits;

@@ -300,6 +300,82 @@ __global__ void reduce3_kernel(const double* __restrict__ part, int C, int S, fl
   if (o2) o2[c] = accumulate ? o2[c] + (float)d : (float)d;
 }
 
+// Fused second stage of the long-row BatchNorm (one launch instead of finalize + apply): block
+// (s, c) merges channel c's S partials itself -- the same Chan merge in the same order as
+// bn_finalize_kernel, so the statistics are bitwise those of the two-launch form -- and
+// normalises its chunk of the row; block (0, c) also stores mean / invstd and the running stats.
+__global__ __launch_bounds__(kNT) void bn_act_apply_stats_kernel(
+    const float* __restrict__ x, long L, int S, const double* __restrict__ part, float* running_mean,
+    float* running_var, float momentum, float eps, float* save_mean, float* save_invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ alpha,
+    float* __restrict__ y) {
+  const int c = blockIdx.y;
+  const double* p = part + (long)c * S * 3;
+  double n = 0, mean = 0, m2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const double nb = p[3 * s], mb = p[3 * s + 1], m2b = p[3 * s + 2];
+    if (nb <= 0) continue;
+    const double nn = n + nb, d = mb - mean;
+    mean += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  const float mu = (float)mean;
+  const float is = (float)(1.0 / sqrt(m2 / (double)L + (double)eps));
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
+  const float ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  const long per = (L + gridDim.x - 1) / gridDim.x;
+  const long lo = blockIdx.x * per, hi = min(L, lo + per);
+  const float* xr = x + (long)c * L;
+  float* yr = y + (long)c * L;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    float z = (xr[i] - mu) * is * ga + be;
+    if (alpha) z = z > 0.f ? z : al * z;
+    yr[i] = z;
+  }
+}
+
+// Fused second stage of the long-row BatchNorm backward (replaces reduce3 + apply): block (s, c)
+// sums channel c's partials in the order reduce3_kernel does, block (0, c) writes the parameter
+// gradients, and every block forms its chunk of gx.
+__global__ __launch_bounds__(kNT) void bn_act_bwd_apply_sums_kernel(
+    const float* __restrict__ gy, const float* __restrict__ x, long L, int S, const double* __restrict__ part,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ alpha, float* gbeta, float* ggamma, float* galpha,
+    int accumulate, float* __restrict__ gx) {
+  const int c = blockIdx.y;
+  const double* p = part + (long)c * S * 3;
+  double a = 0.0, b = 0.0, d = 0.0;
+  for (int s = 0; s < S; ++s) {
+    a += p[3 * s];
+    b += p[3 * s + 1];
+    d += p[3 * s + 2];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    gbeta[c] = accumulate ? gbeta[c] + (float)a : (float)a;
+    ggamma[c] = accumulate ? ggamma[c] + (float)b : (float)b;
+    if (alpha && galpha) galpha[c] = accumulate ? galpha[c] + (float)d : (float)d;
+  }
+  const float invL = 1.f / (float)L;
+  const float sg = (float)a, sgx = (float)b;   // the float sums bn_act_bwd_apply_kernel reads
+  const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  const long per = (L + gridDim.x - 1) / gridDim.x;
+  const long lo = blockIdx.x * per, hi = min(L, lo + per);
+  const float* xr = x + (long)c * L;
+  const float* gr = gy + (long)c * L;
+  float* gxr = gx + (long)c * L;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    const float xh = (xr[i] - mu) * is;
+    float g = gr[i];
+    if (alpha) {
+      const float z = xh * ga + be;
+      if (!(z > 0.f)) g *= al;
+    }
+    gxr[i] = ga * is * (g - sg * invL - xh * sgx * invL);
+  }
+}
+
 // gx = gamma*invstd*(g - sum(g)/L - xhat*sum(g*xhat)/L); the partial sums were reduced into
 // gbeta (= sum g) and ggamma (= sum g*xhat)
 __global__ __launch_bounds__(kNT) void bn_act_bwd_apply_kernel(
@@ -569,10 +645,8 @@ int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const f
   const int S = splits_for(L);
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_partial_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, L, running_mean,
-                     running_var, momentum, eps, save_mean, save_invstd);
-  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, x, C, L, save_mean,
-                     save_invstd, gamma, beta, alpha, y);
+  hipLaunchKernelGGL(bn_act_apply_stats_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part, running_mean,
+                     running_var, momentum, eps, save_mean, save_invstd, gamma, beta, alpha, y);
   return ok(hipGetLastError());
 }
 
@@ -590,11 +664,8 @@ int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const floa
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_act_bwd_partial_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, L, S, save_mean, save_invstd,
                      gamma, beta, alpha, part);
-  float* sums = reinterpret_cast<float*>(part + (size_t)3 * C * S);   // plain sum(g), sum(g*xhat) for gx
-  hipLaunchKernelGGL(reduce3_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, gbeta, ggamma,
-                     alpha ? galpha : nullptr, accumulate, sums, sums + C);
-  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, gy, x, C, L, save_mean,
-                     save_invstd, gamma, beta, alpha, sums, sums + C, gx);
+  hipLaunchKernelGGL(bn_act_bwd_apply_sums_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, L, S, part, save_mean,
+                     save_invstd, gamma, beta, alpha, gbeta, ggamma, galpha, accumulate, gx);
   return ok(hipGetLastError());
 }
 
