@@ -59,6 +59,9 @@ _SIGS = {
     "ganamd_conv_fwd_ex": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp, vp, vp, vp]),
     "ganamd_mix_fwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp]),
     "ganamd_mix_bwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp, vp, vp, vp, vp, vp]),
+    "ganamd_gp_workspace": (c_size_t, [c_int, c_long]),
+    "ganamd_gp_fwd": (c_int, [vp, c_int, c_long, c_float, c_float, c_int, vp, vp, vp, vp]),
+    "ganamd_gp_bwd": (c_int, [vp, vp, vp, c_int, c_long, c_float, c_float, c_int, vp, vp]),
     "ganamd_add_prelu": (c_int, [vp, vp, vp, c_int, c_long, vp, vp]),
     "ganamd_scale_add": (c_int, [vp, vp, vp, c_long, c_long, vp, vp]),
     "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),

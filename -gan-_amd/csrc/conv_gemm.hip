@@ -892,6 +892,16 @@ constexpr int kCUs = 256;
 int num_cus();
 double list_makespan(long F, double L, long R, double d, long slots);
 
+// Price of the extra reduce launch of a split GEMM (its own ~5 us run time on tiny data plus the
+// dependent-launch boundary); GANAMD_REDUCE_US overrides it (tuning experiments).
+double reduce_launch_us() {
+  static const double v = [] {
+    const char* e = getenv("GANAMD_REDUCE_US");
+    return e ? atof(e) : 3.0;
+  }();
+  return v;
+}
+
 // wgrad split-K by a small cost model: a GEMM of `tiles` output tiles, each `kt_total` K-steps of
 // `kflop` FLOPs, runs in ceil(tiles*s / slots) rounds of blocks (slots = resident blocks per CU
 // x CUs) of ceil(kt_total/s) K-steps; splitting adds the slab round trip and a reduce launch.
@@ -906,7 +916,7 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_
     const long per = (kt_total + s - 1) / s;
     const long waves = ((long)tiles * s + slots - 1) / slots;
     double c = (double)waves * per * t_k;
-    if (s > 1) c += 3.0 + (2.0 * s + 1.0) * out_elems * 4.0 / 4e12 * 1e6;
+    if (s > 1) c += reduce_launch_us() + (2.0 * s + 1.0) * out_elems * 4.0 / 4e12 * 1e6;
     return c;
   };
   int best = 1;
@@ -1063,7 +1073,7 @@ ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16
     double c = list_makespan(F, kt_total + ovh, R, per + ovh, slots);
     if (Sx > 1 && R > 0) {
       const long tail_cols = N - (long)nf * pl.bn;
-      c += (3.0 + (2.0 * Sx + 1.0) * (double)M * tail_cols * 4.0 / 4e12 * 1e6) / t_k;
+      c += (reduce_launch_us() + (2.0 * Sx + 1.0) * (double)M * tail_cols * 4.0 / 4e12 * 1e6) / t_k;
     }
     *per_out = per;
     return c;

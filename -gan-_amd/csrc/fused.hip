@@ -185,9 +185,99 @@ void launch_mix_bwd(const Ptr4& f, const float* att, long planes, long HW, const
   hipLaunchKernelGGL((mix_bwd_kernel<M>), dim3(blocks), dim3(kNT), 0, st, f, att, planes, HW, g, gf, gatt);
 }
 
+// ---------------------------------------------------------------- gradient penalty
+// GP = lambda * mean_b (||g_b|| - center)^2 over g = grad_x D(x_hat) [B][n]
+// (train/wgangp.py:34-54, lambda 10 at :68; R1/R2 of wganlazygpR2.py use the squared norm
+// without the root: mode 1).  Pass 1: per-(sample, chunk) double partial sums of g^2; pass 2
+// (one block): the norms and the penalty.  The backward is one elementwise pass:
+//   dGP/dg = gout * lambda * 2 (||g_b|| - center) / (B ||g_b||) * g      (mode 0)
+//   dR/dg  = gout * lambda * 2 / B * g                                   (mode 1)
+constexpr long kGpChunk = 4096;
+
+__global__ __launch_bounds__(kNT) void gp_partial_kernel(const float* __restrict__ g, long n, int S,
+                                                         double* __restrict__ part) {
+  __shared__ double sh[4];
+  const int b = blockIdx.y, s = blockIdx.x;
+  const long per = (n + S - 1) / S;
+  const long lo = s * per, hi = min(n, lo + per);
+  const float* row = g + (long)b * n;
+  double acc = 0.0;
+  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+    const double v = row[i];
+    acc += v * v;
+  }
+  // block sum (4 waves)
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(long)b * S + s] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ __launch_bounds__(kNT) void gp_finalize_kernel(const double* __restrict__ part, int B, int S, float center,
+                                                          float lambda, int mode, float* __restrict__ norms,
+                                                          float* __restrict__ out) {
+  __shared__ double sh[kNT];
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < B; b += kNT) {
+    double sq = 0.0;
+    for (int s = 0; s < S; ++s) sq += part[(long)b * S + s];
+    const double nb = mode == 0 ? sqrt(sq) : sq;
+    norms[b] = (float)nb;
+    acc += mode == 0 ? (nb - center) * (nb - center) : nb;
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < kNT; ++i) t += sh[i];
+    out[0] = (float)(lambda * t / B);
+  }
+}
+
+__global__ __launch_bounds__(kNT) void gp_backward_kernel(const float* __restrict__ g, const float* __restrict__ norms,
+                                                          const float* __restrict__ gout, long n, int B, float center,
+                                                          float lambda, int mode, float* __restrict__ dg) {
+  const long total = (long)B * n;
+  const float go = gout[0];
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < total; i += (long)gridDim.x * kNT) {
+    const int b = (int)(i / n);
+    float k;
+    if (mode == 0) {
+      const float nb = norms[b];
+      k = nb > 0.f ? go * lambda * 2.f * (nb - center) / ((float)B * nb) : 0.f;
+    } else {
+      k = go * lambda * 2.f / (float)B;
+    }
+    dg[i] = k * g[i];
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t ganamd_gp_workspace(int B, long n) {
+  const long S = std::min<long>(64, std::max<long>(1, (n + kGpChunk - 1) / kGpChunk));
+  return sizeof(double) * (size_t)B * S;
+}
+
+int ganamd_gp_fwd(const float* g, int B, long n, float center, float lambda, int mode, float* norms, float* out,
+                  void* workspace, hipStream_t st) {
+  if (!g || !norms || !out || !workspace || B <= 0 || n <= 0 || (mode != 0 && mode != 1)) return GANAMD_EINVAL;
+  const int S = (int)std::min<long>(64, std::max<long>(1, (n + kGpChunk - 1) / kGpChunk));
+  double* part = static_cast<double*>(workspace);
+  hipLaunchKernelGGL(gp_partial_kernel, dim3(S, B), dim3(kNT), 0, st, g, n, S, part);
+  hipLaunchKernelGGL(gp_finalize_kernel, dim3(1), dim3(kNT), 0, st, part, B, S, center, lambda, mode, norms, out);
+  return ok(hipGetLastError());
+}
+
+int ganamd_gp_bwd(const float* g, const float* norms, const float* gout, int B, long n, float center, float lambda,
+                  int mode, float* dg, hipStream_t st) {
+  if (!g || !norms || !gout || !dg || B <= 0 || n <= 0 || (mode != 0 && mode != 1)) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(gp_backward_kernel, dim3(grid_for((long)B * n)), dim3(kNT), 0, st, g, norms, gout, n, B, center,
+                     lambda, mode, dg);
+  return ok(hipGetLastError());
+}
 
 int ganamd_mix_fwd(int M, const float* f0, const float* f1, const float* f2, const float* f3, const float* att,
                    long planes, long HW, float* y, hipStream_t st) {

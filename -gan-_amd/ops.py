@@ -707,6 +707,46 @@ def modconv(x, s, w, geo, c):
 
 
 # ------------------------------------------------------------------------------------------
+# gradient penalty on the critic's input gradient (csrc/fused.hip)
+# ------------------------------------------------------------------------------------------
+
+
+class GradPenalty(Function):
+    """lambda * mean_b (||g_b|| - center)^2 (mode 0: WGAN-GP, train/wgangp.py:34-54) or
+    lambda * mean_b ||g_b||^2 (mode 1: R1/R2, train/wganlazygpR2.py:57-70) of g = grad_x D [B, ...].
+    The penalty and its gradient w.r.t. g come from two fused kernels (ganamd_gp_fwd/_bwd) in
+    closed form; the double backward then continues through the critic's backward operators."""
+
+    @staticmethod
+    def forward(ctx, g, center, lam, mode):
+        g = _c(g)
+        B = g.shape[0]
+        n = g.numel() // B
+        norms = torch.empty(B, device=g.device, dtype=torch.float32)
+        out = torch.empty((), device=g.device, dtype=torch.float32)
+        ws = workspace(LIB.ganamd_gp_workspace(B, n), g.device)
+        check(LIB.ganamd_gp_fwd(ptr(g), B, n, float(center), float(lam), int(mode), ptr(norms), ptr(out), ptr(ws),
+                                stream()), "gp_fwd")
+        ctx.save_for_backward(g, norms)
+        ctx.args = (B, n, float(center), float(lam), int(mode))
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        g, norms = ctx.saved_tensors
+        B, n, center, lam, mode = ctx.args
+        dg = torch.empty_like(g)
+        check(LIB.ganamd_gp_bwd(ptr(g), ptr(norms), ptr(_c(gout.reshape(1))), B, n, center, lam, mode, ptr(dg),
+                                stream()), "gp_bwd")
+        return dg, None, None, None
+
+
+def grad_penalty(g, center=1.0, lam=1.0, mode=0):
+    return GradPenalty.apply(g, center, lam, mode)
+
+
+# ------------------------------------------------------------------------------------------
 # fused per-plane elementwise ops (csrc/fused.hip)
 # ------------------------------------------------------------------------------------------
 

@@ -23,6 +23,7 @@ import contextlib
 
 import torch
 
+from . import ops
 from .checkpoint import CheckpointMixin
 from .optim import FusedAdamW
 from .rng import DeviceRNG
@@ -95,7 +96,11 @@ class Train(CheckpointMixin):
         x_interp = ((1 - eps) * x_real + eps * x_fake).detach()
         x_interp.requires_grad_()
         d_out = self.discriminator(x_interp)
-        return (self.compute_grad2(d_out, x_interp).sqrt() - center).pow(2).mean()
+        # (compute_grad2(d_out, x_interp).sqrt() - center).pow(2).mean(), with the norm, the
+        # penalty and its gradient in two fused kernels (ops.GradPenalty)
+        grad = torch.autograd.grad(outputs=d_out.sum(), inputs=x_interp, create_graph=True, retain_graph=True,
+                                   only_inputs=True)[0]
+        return ops.grad_penalty(grad, center, 1.0, 0)
 
     def compute_grad2(self, d_out, x_in):
         """train/wgangp.py:45-54."""

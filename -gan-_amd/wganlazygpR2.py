@@ -81,12 +81,13 @@ class Train(wgangp.Train):
         x = torch.cat([images, gen_imgs, x_interp]).detach().requires_grad_()
         pred = self.discriminator(x, segments=3)
         grad = torch.autograd.grad(pred.sum(), x, create_graph=True, retain_graph=True, only_inputs=True)[0]
-        g2 = grad.pow(2).view(3 * b_size, -1).sum(1)
         real_loss = -torch.mean(pred[:b_size])
         fake_loss = torch.mean(pred[b_size:2 * b_size])
-        r2_reg_r = REG_WEIGHT * g2[:b_size].mean()
-        r2_reg_f = REG_WEIGHT * g2[b_size:2 * b_size].mean()
-        gp = GP_LAMBDA * (g2[2 * b_size:].sqrt() - 1.0).pow(2).mean() * REG_WEIGHT
+        # R1 = 5 mean |g|^2 (real), R2 = 5 mean |g|^2 (fake), GP = 10 * 5 mean (|g| - 1)^2 (interp):
+        # each one fused kernel pair (ops.GradPenalty) on its contiguous batch slice of the gradient
+        r2_reg_r = ops.grad_penalty(grad[:b_size], 0.0, float(REG_WEIGHT), 1)
+        r2_reg_f = ops.grad_penalty(grad[b_size:2 * b_size], 0.0, float(REG_WEIGHT), 1)
+        gp = ops.grad_penalty(grad[2 * b_size:], 1.0, float(GP_LAMBDA * REG_WEIGHT), 0)
         (real_loss + fake_loss + r2_reg_r + r2_reg_f + gp).backward()
         return real_loss, fake_loss, gp, r2_reg_r, r2_reg_f
 

@@ -237,6 +237,18 @@ int ganamd_add_prelu(const float* a, const float* b, const float* alpha, int C, 
 int ganamd_scale_add(const float* x, const float* s, const float* r, long planes, long HW, float* y,
                      hipStream_t stream);
 
+/* Gradient penalty on the critic's input gradient g = grad_x D(x_hat), [B][n] (n = 3*64*64):
+ *   mode 0 (WGAN-GP, train/wgangp.py:34-54,68):  out = lambda * mean_b (||g_b||_2 - center)^2
+ *   mode 1 (R1 / R2, train/wganlazygpR2.py:57-70): out = lambda * mean_b ||g_b||_2^2
+ * norms[b] receives ||g_b|| (mode 0) or ||g_b||^2 (mode 1).  ganamd_gp_bwd: dg = d out / d g
+ * scaled by gout[0] (device scalar), from g and the saved norms -- the closed form, no autograd
+ * graph of the penalty itself.  Workspace: ganamd_gp_workspace(B, n) bytes. */
+size_t ganamd_gp_workspace(int B, long n);
+int ganamd_gp_fwd(const float* g, int B, long n, float center, float lambda, int mode, float* norms, float* out,
+                  void* workspace, hipStream_t stream);
+int ganamd_gp_bwd(const float* g, const float* norms, const float* gout, int B, long n, float center, float lambda,
+                  int mode, float* dg, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Real-data input pipeline (units/dataloader.py:5-14): a batch of B
  * decoded images u8 [B][H][W][3] (one size) -> f32 NCHW [B][3][OH][OW]:

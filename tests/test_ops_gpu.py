@@ -559,3 +559,19 @@ def test_conv_bf16_math(ops, case):
     for ref, a32, a16 in zip((y, gx, gw), got["fp32"], got["bf16"]):
         e32, e16 = rel(a32, ref), rel(a16, ref)
         assert e32 < 1e-5 and 3e-4 < e16 < 1e-2, (e32, e16)
+
+
+@pytest.mark.parametrize("mode,center,lam", [(0, 1.0, 10.0), (1, 0.0, 5.0)])
+def test_grad_penalty_fused(ops, mode, center, lam):
+    """ganamd_gp_fwd/_bwd: the penalty of train/wgangp.py:34-54 (mode 0) and R1/R2 of
+    wganlazygpR2.py:57-70 (mode 1) and its gradient w.r.t. the input gradient, vs float64."""
+    g64 = (torch.randn(6, 3, 64, 64, generator=torch.Generator().manual_seed(7 + mode), dtype=torch.float64)
+           * 0.02).requires_grad_()
+    sq = g64.pow(2).view(6, -1).sum(1)
+    ref = lam * ((sq.sqrt() - center).pow(2).mean() if mode == 0 else sq.mean())
+    (want,) = torch.autograd.grad(ref * 0.7, g64)
+    g = g64.detach().float().to(DEV).requires_grad_()
+    out = ops.grad_penalty(g, center, lam, mode)
+    assert abs(float(out) - float(ref)) / abs(float(ref)) < 1e-6
+    (got,) = torch.autograd.grad(out * 0.7, g)
+    assert rel(got, want) < 1e-6
