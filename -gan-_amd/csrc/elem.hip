@@ -545,42 +545,94 @@ __global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int
 }
 
 // ---------------------------------------------------------------- separable resampling
-// Separable resampling through LDS: a workgroup stages `ppb` whole input planes, applies the
+// Separable resampling through LDS: a workgroup stages `ppb` whole input planes (16-byte loads)
+// and the two ELL tap tables (KR/KC taps per output row/column, zero-weight padding), applies the
 // column table along rows into an LDS intermediate [IH][OW], then the row table along columns
-// straight to global memory.  HBM traffic = one read of x + one write of y; the tap tables
-// (ELL: KR/KC taps per output row/column, zero-weight padding) stay in L1.
+// straight to global memory.  HBM traffic = one read of x + one write of y.  Each thread owns V
+// consecutive output columns (V = 4 when OW % 4 == 0: 16-byte LDS/global stores) and walks rows
+// with a fixed stride, so there is no per-element index division.
+inline __host__ __device__ int align4(int n) { return (n + 3) & ~3; }
+
+template <int V>
 __global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict__ x, long planes, int IH, int IW,
                                                          float* __restrict__ y, int OH, int OW,
                                                          const int32_t* __restrict__ ri, const float* __restrict__ rw,
                                                          int KR, const int32_t* __restrict__ ci,
                                                          const float* __restrict__ cw, int KC, int ppb) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
   extern __shared__ float lds[];
   const long p0 = (long)blockIdx.x * ppb;
   const int np = (int)min((long)ppb, planes - p0);
-  float* xs = lds;
-  float* ts = lds + ppb * IH * IW;
+  float* xs = lds;                                  // [ppb][IH][IW]
+  float* ts = xs + align4(ppb * IH * IW);           // [ppb][IH][OW]
+  float* cws = ts + align4(ppb * IH * OW);          // [OW][KC]
+  int* cis = reinterpret_cast<int*>(cws + OW * KC);
+  float* rws = reinterpret_cast<float*>(cis + OW * KC);   // [OH][KR]
+  int* ris = reinterpret_cast<int*>(rws + OH * KR);
+  const int tid = threadIdx.x;
   const int nin = np * IH * IW;
   const float* xg = x + p0 * IH * IW;
-  for (int i = threadIdx.x; i < nin; i += kNT) xs[i] = xg[i];
-  __syncthreads();
-  const int nt = np * IH * OW;
-  for (int i = threadIdx.x; i < nt; i += kNT) {
-    const int ow = i % OW, r = i / OW;
-    const float* xr = xs + r * IW;
-    float acc = 0.f;
-    for (int b = 0; b < KC; ++b) acc += cw[ow * KC + b] * xr[ci[ow * KC + b]];
-    ts[i] = acc;
+  if (((IH * IW) & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    for (int i = tid; i < nin / 4; i += kNT)
+      reinterpret_cast<f4*>(xs)[i] = reinterpret_cast<const f4*>(xg)[i];
+  } else {
+    for (int i = tid; i < nin; i += kNT) xs[i] = xg[i];
+  }
+  for (int i = tid; i < OW * KC; i += kNT) {
+    cws[i] = cw[i];
+    cis[i] = ci[i];
+  }
+  for (int i = tid; i < OH * KR; i += kNT) {
+    rws[i] = rw[i];
+    ris[i] = ri[i];
   }
   __syncthreads();
-  const int ohw = OH * OW, no = np * ohw;
-  float* yg = y + p0 * ohw;
-  for (int i = threadIdx.x; i < no; i += kNT) {
-    const int ow = i % OW, r = i / OW;
-    const int oh = r % OH, pl = r / OH;
-    const float* tp = ts + pl * IH * OW + ow;
-    float acc = 0.f;
-    for (int a = 0; a < KR; ++a) acc += rw[oh * KR + a] * tp[ri[oh * KR + a] * OW];
-    yg[i] = acc;
+  const int QW = OW / V;                  // column groups per row (host: QW <= kNT)
+  const int q = tid % QW, r0 = tid / QW, rstep = kNT / QW;
+  const bool active = r0 < rstep;         // threads past rstep*QW sit out
+  if (active) {
+    for (int r = r0; r < np * IH; r += rstep) {
+      const float* xr = xs + r * IW;
+      float acc[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int o = (q * V + v) * KC;
+        float s = 0.f;
+        for (int b = 0; b < KC; ++b) s += cws[o + b] * xr[cis[o + b]];
+        acc[v] = s;
+      }
+      float* t = ts + r * OW + q * V;
+      if constexpr (V == 4)
+        *reinterpret_cast<f4*>(t) = f4{acc[0], acc[1], acc[2], acc[3]};
+      else
+        t[0] = acc[0];
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  float* yg = y + p0 * OH * OW;
+  for (int rr = r0; rr < np * OH; rr += rstep) {
+    const int pl = rr / OH, oh = rr - pl * OH;
+    const float* tp = ts + pl * IH * OW + q * V;
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    for (int a = 0; a < KR; ++a) {
+      const float w = rws[oh * KR + a];
+      const float* t = tp + ris[oh * KR + a] * OW;
+      if constexpr (V == 4) {
+        const f4 u = *reinterpret_cast<const f4*>(t);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[v] += w * u[v];
+      } else {
+        acc[0] += w * t[0];
+      }
+    }
+    float* o = yg + (long)rr * OW + q * V;
+    if constexpr (V == 4)
+      *reinterpret_cast<f4*>(o) = f4{acc[0], acc[1], acc[2], acc[3]};
+    else
+      o[0] = acc[0];
   }
 }
 
@@ -700,14 +752,24 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
 int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
                       const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t st) {
   if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;
-  // planes per workgroup: >= ~2K staged inputs, LDS <= 48 KB (3 workgroups per CU)
+  // planes per workgroup: ~2K staged inputs but <= ~8K outputs (an upsampling adjoint such as
+  // pool5's 5x5 -> 64x64 would otherwise pack 81 planes, 330K outputs, into each of a few dozen
+  // workgroups), LDS <= 48 KB (3 workgroups per CU)
+  const int V = (OW % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 4 : 1;
+  if (OW / V > kNT || IH <= 0 || IW <= 0 || OH <= 0 || OW <= 0) return GANAMD_EINVAL;
   const long per_plane = (long)IH * IW + (long)IH * OW;
-  if (per_plane * 4 > 48 * 1024) return GANAMD_EINVAL;
-  int ppb = (int)std::max<long>(1, 2048 / ((long)IH * IW));
-  ppb = (int)std::min<long>(ppb, (48 * 1024) / (4 * per_plane));
+  const long tab = 2L * ((long)OW * KC + (long)OH * KR) + 8;   // tables + alignment slack (floats)
+  if ((per_plane + tab) * 4 > 48 * 1024) return GANAMD_EINVAL;
+  int ppb = (int)std::max<long>(1, std::min<long>(2048 / ((long)IH * IW), 8192 / ((long)OH * OW)));
+  ppb = (int)std::min<long>(ppb, (48 * 1024 / 4 - tab) / per_plane);
   const long blocks = (planes + ppb - 1) / ppb;
-  hipLaunchKernelGGL(resample2d_kernel, dim3((unsigned)blocks), dim3(kNT), (size_t)(4 * ppb * per_plane), st, x,
-                     planes, IH, IW, y, OH, OW, ri, rw, KR, ci, cw, KC, ppb);
+  const size_t bytes = 4 * (size_t)(align4(ppb * IH * IW) + align4(ppb * IH * OW) + 2 * (OW * KC + OH * KR));
+  if (V == 4)
+    hipLaunchKernelGGL(resample2d_kernel<4>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, planes, IH, IW, y, OH,
+                       OW, ri, rw, KR, ci, cw, KC, ppb);
+  else
+    hipLaunchKernelGGL(resample2d_kernel<1>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, planes, IH, IW, y, OH,
+                       OW, ri, rw, KR, ci, cw, KC, ppb);
   return ok(hipGetLastError());
 }
 

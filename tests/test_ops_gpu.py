@@ -261,11 +261,15 @@ def test_conv_prelu_double_backward(ops):
     assert rel(got[0], want[0]) < 1e-4
 
 
-@pytest.mark.parametrize("kind,n", [("smooth", 64), ("up2_smooth", 8), ("smooth_down2", 32), ("pool5", 16)])
-def test_resample_and_adjoint(ops, kind, n):
+@pytest.mark.parametrize("kind,n,planes", [("smooth", 64, 15), ("up2_smooth", 8, 15), ("smooth_down2", 32, 15),
+                                           ("pool5", 16, 15), ("pool5", 64, 101), ("up2_smooth", 32, 67),
+                                           ("smooth_down2", 64, 33), ("smooth", 5, 250), ("smooth", 6, 9)])
+def test_resample_and_adjoint(ops, kind, n, planes):
+    """Both directions (forward table and adjoint) against the dense float64 operator; plane
+    counts that leave a ragged last workgroup, 5- and 6-wide maps (the one-column path)."""
     from gan_amd import tables
     g = torch.Generator().manual_seed(n)
-    x = torch.randn(3, 5, n, n, generator=g, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(planes, 1, n, n, generator=g, dtype=torch.float64, requires_grad=True)
     m = torch.from_numpy(tables.operator_1d(kind, n))
     y = torch.einsum("oh,pw,bchw->bcop", m, m, x)
     gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
