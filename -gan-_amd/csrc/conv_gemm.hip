@@ -801,15 +801,18 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
 
 // Sum the replication-padded dgrad image back onto the edge pixels (ReplicationPad2d backward),
 // or crop it for zero padding.  xp: [C*B][Hp][Wp] -> x: [C*B][H][W].
+// I: index type (32-bit whenever the tensor allows it: 64-bit division is a long software sequence).
+template <typename I>
 __global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict__ x, long planes, int H, int W,
                                 int pad, int replicate) {
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  const long total = planes * H * W;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W;
-    const int h = (i / W) % H;
-    const long pl = i / ((long)H * W);
-    const float* s = xp + pl * Hp * Wp;
+  const I total = (I)(planes * H * W);
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    const I r = i / (I)W;
+    const int w = (int)(i - r * (I)W);
+    const I pl = r / (I)H;
+    const int h = (int)(r - pl * (I)H);
+    const float* s = xp + (long)pl * Hp * Wp;
     if (!replicate) {
       x[i] = s[(h + pad) * Wp + (w + pad)];
       continue;
@@ -829,16 +832,20 @@ __global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict_
 // stride-2 tap of the wrong parity), a run of outputs at a replication-padded edge.  Input row i
 // is read by output row oh through tap kh iff clamp(oh*s - pad + kh) lies in [lo, hi], where
 // lo = hi = i, except that a replicated edge row also takes every position beyond the edge.
+template <typename I>
 __global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict__ gx, int C, int B, int H, int W,
                                   int OH, int OW, int KH, int KW, int stride, int pad, int replicate) {
-  const long total = (long)C * B * H * W;
+  const I total = (I)C * B * H * W;
   const int T = KH * KW;
   constexpr int kFar = 1 << 20;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int j = (int)(idx % W);
-    const int i = (int)((idx / W) % H);
-    const int b = (int)((idx / ((long)W * H)) % B);
-    const int c = (int)(idx / ((long)W * H * B));
+  for (I idx = blockIdx.x * (I)blockDim.x + threadIdx.x; idx < total; idx += (I)gridDim.x * blockDim.x) {
+    const I r1 = idx / (I)W;
+    const int j = (int)(idx - r1 * (I)W);
+    const I r2 = r1 / (I)H;
+    const int i = (int)(r1 - r2 * (I)H);
+    const I c_ = r2 / (I)B;
+    const int b = (int)(r2 - c_ * (I)B);
+    const int c = (int)c_;
     const int ilo = (replicate && i == 0) ? -kFar : i, ihi = (replicate && i == H - 1) ? kFar : i;
     const int jlo = (replicate && j == 0) ? -kFar : j, jhi = (replicate && j == W - 1) ? kFar : j;
     float acc = 0.f;
@@ -1553,8 +1560,13 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     p.ohw = d->OH * d->OW;
     if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
     const long total = (long)d->Cin * d->B * d->H * d->W;
-    hipLaunchKernelGGL(dgrad_fold_kernel, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H, d->W,
-                       d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
+    const int rep = d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0;
+    if (total < (1L << 31) - (1L << 24))
+      hipLaunchKernelGGL(dgrad_fold_kernel<unsigned>, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B,
+                         d->H, d->W, d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, rep);
+    else
+      hipLaunchKernelGGL(dgrad_fold_kernel<long>, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H,
+                         d->W, d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, rep);
     return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   if (d->transposed) {
@@ -1573,8 +1585,14 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
   if (pad_bytes) {
     const long planes = (long)d->Cin * d->B;
-    hipLaunchKernelGGL(fold_pad_kernel, dim3(grid1d(planes * d->H * d->W)), dim3(256), 0, stream, out, gx, planes,
-                       d->H, d->W, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0);
+    const long total = planes * d->H * d->W;
+    const int rep = d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0;
+    if (total < (1L << 31) - (1L << 24))
+      hipLaunchKernelGGL(fold_pad_kernel<unsigned>, dim3(grid1d(total)), dim3(256), 0, stream, out, gx, planes, d->H,
+                         d->W, d->pad, rep);
+    else
+      hipLaunchKernelGGL(fold_pad_kernel<long>, dim3(grid1d(total)), dim3(256), 0, stream, out, gx, planes, d->H, d->W,
+                         d->pad, rep);
     if (hipGetLastError() != hipSuccess) return GANAMD_ELAUNCH;
   }
   return GANAMD_OK;
