@@ -419,13 +419,38 @@ __global__ __launch_bounds__(kNT) void prelu_bwd_kernel(const float* __restrict_
   const float al = a[c];
   const long base = (long)c * L;
   float acc = 0.f;
-  for (long i = lo + threadIdx.x; i < hi; i += kNT) {
-    const float v = x[base + i], g = gy[base + i];
-    if (v > 0.f) {
-      if (gx) gx[base + i] = g;
-    } else {
-      if (gx) gx[base + i] = al * g;
-      acc += g * v;
+  const bool vec = (L & 3) == 0 && ((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(x) |
+                                     reinterpret_cast<uintptr_t>(gx)) & 15) == 0;
+  if (vec) {   // 16-byte accesses; the block's range in whole float4s
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const long L4 = L / 4, per4 = (L4 + S - 1) / S;
+    const long lo4 = s * per4, hi4 = min(L4, lo4 + per4);
+    const f4* x4 = reinterpret_cast<const f4*>(x + base);
+    const f4* g4 = reinterpret_cast<const f4*>(gy + base);
+    f4* o4 = gx ? reinterpret_cast<f4*>(gx + base) : nullptr;
+    for (long i = lo4 + threadIdx.x; i < hi4; i += kNT) {
+      const f4 v = x4[i], g = g4[i];
+      f4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (v[j] > 0.f) {
+          o[j] = g[j];
+        } else {
+          o[j] = al * g[j];
+          acc += g[j] * v[j];
+        }
+      }
+      if (o4) o4[i] = o;
+    }
+  } else {
+    for (long i = lo + threadIdx.x; i < hi; i += kNT) {
+      const float v = x[base + i], g = gy[base + i];
+      if (v > 0.f) {
+        if (gx) gx[base + i] = g;
+      } else {
+        if (gx) gx[base + i] = al * g;
+        acc += g * v;
+      }
     }
   }
   if (part) {
