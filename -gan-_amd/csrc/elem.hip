@@ -408,6 +408,21 @@ __global__ __launch_bounds__(kNT) void prelu_fwd_kernel(const float* __restrict_
   }
 }
 
+// Rows of a multiple of 4 elements: 16-byte accesses, 32-bit index arithmetic (n4 < 2^29).
+__global__ __launch_bounds__(kNT) void prelu_fwd_vec_kernel(const float* __restrict__ x, const float* __restrict__ a,
+                                                            unsigned n4, unsigned L4, float* __restrict__ y) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const f4* x4 = reinterpret_cast<const f4*>(x);
+  f4* y4 = reinterpret_cast<f4*>(y);
+  for (unsigned i = blockIdx.x * kNT + threadIdx.x; i < n4; i += gridDim.x * kNT) {
+    const float al = a[i / L4];
+    f4 v = x4[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : al * v[j];
+    y4[i] = v;
+  }
+}
+
 // gx (optional) and per-block partials of galpha = sum gy*x over x<=0
 __global__ __launch_bounds__(kNT) void prelu_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
                                                         const float* __restrict__ a, long L, int S,
@@ -748,7 +763,12 @@ int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const floa
 
 int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y, hipStream_t st) {
   if (!x || !alpha || !y || C <= 0 || L <= 0) return GANAMD_EINVAL;
-  hipLaunchKernelGGL(prelu_fwd_kernel, dim3(grid_for((long)C * L)), dim3(kNT), 0, st, x, alpha, C, L, y);
+  const long n = (long)C * L;
+  if ((L & 3) == 0 && n < (1L << 31) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0)
+    hipLaunchKernelGGL(prelu_fwd_vec_kernel, dim3(grid_for(n / 4)), dim3(kNT), 0, st, x, alpha, (unsigned)(n / 4),
+                       (unsigned)(L / 4), y);
+  else
+    hipLaunchKernelGGL(prelu_fwd_kernel, dim3(grid_for(n)), dim3(kNT), 0, st, x, alpha, C, L, y);
   return ok(hipGetLastError());
 }
 
