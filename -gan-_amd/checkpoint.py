@@ -16,8 +16,13 @@ moments and step counters are saved too.  Everything is tensors/str/int, so
 from __future__ import annotations
 
 import os
+import pickle
 
 import torch
+
+
+def _is_dist():
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
 
 
 def _cpu_state(module):
@@ -45,8 +50,10 @@ class CheckpointMixin:
                  "discriminator": _cpu_state(self.discriminator), "discriminator_name": self.discriminator_name,
                  "method": train_name, "epoch": e, "i": ii,
                  "optimizer_G": self.optimizer_G.state_dict(), "optimizer_D": self.optimizer_D.state_dict()}
-        os.makedirs(self.ckpt_root, exist_ok=True)
         path = ckpt_path(self.ckpt_root, self.generator_name, self.discriminator_name, train_name, e, ii)
+        if _is_dist() and torch.distributed.get_rank() != 0:
+            return path          # data parallel: the replicas are identical, rank 0 writes the file
+        os.makedirs(self.ckpt_root, exist_ok=True)
         torch.save(state, path)
         return path
 
@@ -54,7 +61,14 @@ class CheckpointMixin:
         path = os.path.join(self.ckpt_root, name + ".pth")
         if not os.path.isfile(path):
             return None
-        return torch.load(path, map_location="cpu", weights_only=True)
+        try:
+            return torch.load(path, map_location="cpu", weights_only=True)
+        except pickle.UnpicklingError as e:
+            raise RuntimeError(
+                f"{path}: not a state_dict checkpoint.  The reference's train/trainunits.py:58-76 pickles whole "
+                "nn.Module objects, which are never unpickled here (weights_only=True).  Convert it once where the "
+                "reference is importable: ck['generator'] = ck['generator'].state_dict() (same for "
+                "'discriminator') and torch.save(ck, path).") from e
 
     def load_generator_ckpt(self, name):
         """trainunits.py:93-111: also restores epoch / i; loads in place."""

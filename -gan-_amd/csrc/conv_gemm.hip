@@ -348,9 +348,6 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
   int sp = tap();
 
   auto gload = [&](int kt) {
-#ifdef GANAMD_EXP_NOLOAD   // timing experiment only: operands stop changing after the first K-steps
-    if (kt > kt0 + 1) return;
-#endif
 #pragma unroll
     for (int e = 0; e < EA; ++e)
       if (tid + e * kThreads < A4) ra[e] = bload4(rw, a_off[e] + kt * (BK * 4));
@@ -436,171 +433,6 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
         float v = p.alpha * acc[i][j][r];
-        if (finish) {
-          if (p.oscale) v *= p.oscale[m * g.B + b];
-          if (p.bias) v += p.bias[m];
-          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.N + n];
-          if (p.act) v = v > 0.f ? v : p.act[m] * v;
-        }
-        out[(long)m * ldo + n] = v;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Direct variant: no LDS, no barriers.  Each wave owns a (32*TM) x (32*TN) output tile and loads
-// its MFMA operands straight into registers: with the k-permuted 32x32x2 layout, lane (r, h)
-// needs A[row r][k = 8h .. 8h+7] (32 contiguous bytes of the packed weight row: two 16-byte
-// loads) and B[k = 8h .. 8h+7][pixel r] (8 channel rows of the gathered source at one pixel:
-// 8 dword loads, coalesced across the 32 pixels of a half-wave).  The operands of K-step kt+1
-// are loaded into a second register set while the MFMAs of K-step kt run, so the only waits are
-// the compiler's counted vmcnt on loads issued a whole K-step earlier; the 4 waves of a block
-// share the A rows (and the taps' overlapping pixels) through L1 instead of LDS.
-template <int TM, int TN, int MODE, bool BSCALE>
-__global__ __launch_bounds__(kThreads) void conv_direct_kernel(ConvArgs p) {
-  constexpr int BM = 32 * TM, BN = 4 * 32 * TN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int nct = p.Ckp / BK;
-  const int kt_total = nct * p.T;
-  int tx, ty, kt0, kt1, split = -1;
-  {
-    const int bid = blockIdx.x;
-    if (bid < p.full_blocks) {
-      ty = bid % p.gy;
-      tx = bid / p.gy;
-      kt0 = 0;
-      kt1 = kt_total;
-    } else {
-      const int t = bid - p.full_blocks;
-      const int rr = t / p.S;
-      split = t - rr * p.S;
-      ty = rr % p.gy;
-      tx = p.nfull_t + rr / p.gy;
-      kt0 = split * p.kt_per_split;
-      kt1 = min(kt_total, kt0 + p.kt_per_split);
-    }
-  }
-  const int m0 = ty * BM;
-  const int nw0 = tx * BN + wave * (32 * TN);   // this wave's first pixel
-  const Gather& g = p.g;
-  const int Krow = p.T * p.Ckp;
-  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
-  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
-  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
-  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
-
-  // per fragment j: this lane's pixel
-  int img[TN], poh[TN], pow_[TN], pb[TN];
-  bool pok[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = nw0 + j * 32 + r;
-    pok[j] = n < p.N;
-    const int nn = pok[j] ? n : 0;
-    pb[j] = nn / p.ohw;
-    const int rr = nn - pb[j] * p.ohw;
-    poh[j] = rr / g.OW;
-    pow_[j] = rr - poh[j] * g.OW;
-    img[j] = pb[j] * g.H * g.W;
-  }
-  // A: row m0 + i*32 + r, k = kt*16 + 8h .. +7  (packed rows are padded to the tile grid)
-  int a_off[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) a_off[i] = 4 * ((m0 + i * 32 + r) * Krow + 8 * h);
-
-  int cc = kt0 / p.T, kh, kw;
-  {
-    const int t = kt0 - cc * p.T;
-    kh = t / g.KW;
-    kw = t - kh * g.KW;
-  }
-
-  f32x4 ra[2][TM][2];
-  float rb[2][TN][8], rs[2][TN][8];
-  auto gload = [&](int kt, int buf) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      ra[buf][i][0] = bload4(rw, a_off[i] + kt * (BK * 4));
-      ra[buf][i][1] = bload4(rw, a_off[i] + kt * (BK * 4) + 16);
-    }
-    const int c = cc * BK + 8 * h;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int sp = pok[j] ? tap_offset<MODE>(g, poh[j], pow_[j], kh, kw) : -1;
-      const unsigned base = sp >= 0 ? 4u * (unsigned)(img[j] + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
-      const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + pb[j]) : (unsigned)kOOB;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        rb[buf][j][e] = bload(rx, (int)(base + (unsigned)e * cs4));
-        if (BSCALE) rs[buf][j][e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
-      }
-    }
-    if (++kw == g.KW) {
-      kw = 0;
-      if (++kh * g.KW >= p.T) {
-        kh = 0;
-        ++cc;
-      }
-    }
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-
-  auto compute = [&](int buf) {
-    float a[TM][8], b[TN][8];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[i][e] = ra[buf][i][0][e];
-        a[i][4 + e] = ra[buf][i][1][e];
-      }
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) b[j][e] = BSCALE ? rb[buf][j][e] * rs[buf][j][e] : rb[buf][j][e];
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-  };
-
-  gload(kt0, 0);
-  int kt = kt0;
-  for (; kt + 2 <= kt1; kt += 2) {
-    gload(kt + 1, 1);
-    compute(0);
-    if (kt + 2 < kt1) gload(kt + 2, 0);
-    compute(1);
-  }
-  if (kt < kt1) compute(0);
-
-  const bool finish = split < 0 || p.S == 1;
-  float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
-  const long ldo = finish ? p.N : p.tail_cols;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = nw0 + j * 32 + r;
-    if (n >= p.N) continue;
-    const int b = (finish && p.oscale) ? n / p.ohw : 0;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = m0 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (m >= p.M) continue;
-        float v = p.alpha * acc[i][j][q];
         if (finish) {
           if (p.oscale) v *= p.oscale[m * g.B + b];
           if (p.bias) v += p.bias[m];
@@ -940,19 +772,9 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_
   return Plan{bm, bn, (kt_total + per - 1) / per, per};
 }
 
-// GANAMD_CONV_KERNEL=lds selects the LDS-staged kernel, =direct the LDS-free one (default).
-int conv_direct() {
-  static const int v = [] {
-    const char* e = getenv("GANAMD_CONV_KERNEL");
-    return (e && e[0] == 'd') ? 1 : 0;   // default: the LDS kernel (direct measured at parity or slower)
-  }();
-  return v;
-}
-constexpr int kDirectTN = 2;
-
 void conv_tile(int M, int* bm, int* bn) {
   *bm = conv_bm(M);
-  *bn = conv_direct() ? 4 * 32 * kDirectTN : conv_bn(*bm, 0);
+  *bn = conv_bn(*bm, 0);
 }
 
 // Resident blocks per CU of a kernel instance (the runtime's occupancy calculator; without a
@@ -980,28 +802,8 @@ int conv_occ() {
   return v;
 }
 
-template <int TM, int MODE, bool BSCALE>
-int direct_occ() {
-  static const int v = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_direct_kernel<TM, kDirectTN, MODE, BSCALE>, kThreads, 0) !=
-            hipSuccess || n <= 0)
-      n = 2;
-    return n;
-  }();
-  return v;
-}
-
 template <int MODE, bool BSCALE, bool BF16>
 int conv_occ_tile(int bm, int bn) {
-  if (conv_direct() && !BF16) {
-    switch (bm) {
-      case 32: return direct_occ<1, MODE, BSCALE>();
-      case 64: return direct_occ<2, MODE, BSCALE>();
-      case 96: return direct_occ<3, MODE, BSCALE>();
-      default: return direct_occ<4, MODE, BSCALE>();
-    }
-  }
   switch (bm) {
     case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE, BF16>();
     case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
@@ -1182,37 +984,8 @@ hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t 
   return hipGetLastError();
 }
 
-template <int TM, int MODE, bool BSCALE>
-hipError_t launch_direct(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t st) {
-  constexpr int BN = 4 * 32 * kDirectTN;
-  p.gy = pl.gy;
-  p.nfull_t = pl.nfull_t;
-  p.full_blocks = pl.nfull_t * pl.gy;
-  p.S = pl.S;
-  p.kt_per_split = pl.kt_per_split;
-  p.tail_n0 = pl.nfull_t * BN;
-  p.tail_cols = std::max(0, p.N - p.tail_n0);
-  p.slab = pl.slab_elems ? slab : nullptr;
-  const long blocks = (long)p.full_blocks + (long)(pl.gx - pl.nfull_t) * pl.gy * pl.S;
-  hipLaunchKernelGGL((conv_direct_kernel<TM, kDirectTN, MODE, BSCALE>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
-                     p);
-  if (pl.slab_elems)
-    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.tail_cols)), dim3(256), 0, st, slab, pl.S,
-                       p.M, p.tail_cols, p.tail_n0, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
-                       p.y);
-  return hipGetLastError();
-}
-
 template <int MODE, bool BSCALE, bool BF16>
 hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab, hipStream_t st) {
-  if (conv_direct() && !BF16) {
-    switch (pl.bm) {
-      case 32: return launch_direct<1, MODE, BSCALE>(p, pl, slab, st);
-      case 64: return launch_direct<2, MODE, BSCALE>(p, pl, slab, st);
-      case 96: return launch_direct<3, MODE, BSCALE>(p, pl, slab, st);
-      default: return launch_direct<4, MODE, BSCALE>(p, pl, slab, st);
-    }
-  }
   switch (pl.bm) {
     case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
@@ -1301,10 +1074,27 @@ hipError_t dispatch_wgrad(const WgradArgs& p, int T, float* slab, hipStream_t st
            : dispatch_wgrad_tile<kZero, false, false>(p, T, pl, slab, st);
 }
 
+// Every tensor a conv call touches is addressed through a buffer descriptor with a 32-bit byte
+// range (and offsets at or past 2^31 are the out-of-range sentinel): reject geometries whose
+// largest operand -- input, output, the padded dgrad frame, the scatter-dgrad tap products, the
+// packed weights -- reaches 2^31 bytes instead of letting an offset wrap.
+bool extents_ok(const ganamd_conv_desc* d) {
+  const long lim = (1L << 31) - 1;
+  const long T = (long)d->KH * d->KW;
+  const long x = 4L * d->Cin * d->B * d->H * d->W;
+  const long y = 4L * d->Cout * d->B * d->OH * d->OW;
+  const long frame = 4L * d->Cin * d->B * (d->H + 2L * d->KH) * (d->W + 2L * d->KW);
+  const long frame_t = 4L * d->Cout * d->B * (d->OH + 2L * d->KH) * (d->OW + 2L * d->KW);
+  const bool scatter = !d->transposed && T > 1 && (d->stride > 1 || (long)d->H * d->W <= 100);   // dgrad_scatter
+  const long taps = scatter ? 4L * d->Cin * T * d->B * d->OH * d->OW : 0;
+  const long wpk = 4L * (d->Cout + 256L) * T * (d->Cin + 64L);
+  return x <= lim && y <= lim && frame <= lim && frame_t <= lim && taps <= lim && wpk <= lim;
+}
+
 bool desc_ok(const ganamd_conv_desc* d) {
   return d && d->B > 0 && d->Cin > 0 && d->Cout > 0 && d->H > 0 && d->W > 0 && d->OH > 0 && d->OW > 0 &&
          d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0 &&
-         (d->math == GANAMD_MATH_F32 || d->math == GANAMD_MATH_BF16);
+         (d->math == GANAMD_MATH_F32 || d->math == GANAMD_MATH_BF16) && extents_ok(d);
 }
 
 }  // namespace

@@ -709,7 +709,12 @@ inline int ok(hipError_t e) { return e == hipSuccess ? GANAMD_OK : GANAMD_ELAUNC
 
 extern "C" {
 
-const char* ganamd_version(void) { return "ganamd 0.1 gfx950"; }
+// GANAMD_SRC_HASH: hash of the sources this library was compiled from (set by
+// __graft_entry__.build(), which rebuilds whenever it differs from the tree's).
+#ifndef GANAMD_SRC_HASH
+#define GANAMD_SRC_HASH "unknown"
+#endif
+const char* ganamd_version(void) { return "ganamd 0.2 gfx950 src:" GANAMD_SRC_HASH; }
 
 int ganamd_stream_capture_id(hipStream_t stream, unsigned long long* capture_id) {
   if (!capture_id) return GANAMD_EINVAL;

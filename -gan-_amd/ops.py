@@ -20,6 +20,7 @@ from dataclasses import dataclass
 import torch
 from torch.autograd import Function
 from torch.autograd.function import once_differentiable
+from torch.autograd.graph import get_gradient_edge
 
 from . import _lib
 from ._lib import LIB, check, iptr, ptr, stream, workspace
@@ -348,6 +349,20 @@ def flat_grad(p):
     return g
 
 
+def wanted(t) -> bool:
+    """Will the backward pass now running use a gradient for ``t``?  False for the critic's
+    weights inside the gradient penalty's ``autograd.grad(d_out.sum(), x_hat, create_graph=True)``
+    (wgangp.py:47): only the input gradient is asked for there, so weight / bias / slope gradients
+    are dead work -- the engine would drop them (torch's own convolution backward skips them by
+    the same test).  They ARE computed in the penalty's second backward, where they are used."""
+    if t is None or not t.requires_grad:
+        return False
+    try:
+        return bool(torch._C._will_engine_execute_node(get_gradient_edge(t).node))
+    except RuntimeError:       # not inside an engine call (a direct .backward() of this node)
+        return True
+
+
 def row_sum_acc(a, out):
     """out[c] += sum over the row c of a (a conv bias gradient into the flat gradient buffer)."""
     a = _c(a)
@@ -375,13 +390,13 @@ class ConvFwd(Function):
         wv = ctx.w_arg if ctx.w_arg.is_contiguous() else w     # the Parameter itself where possible
         gx = ConvDgrad.apply(gy, wv, geo, alpha) if ctx.needs_input_grad[0] else None
         gw = gb = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and wanted(ctx.w_arg):
             tgt = flat_grad(ctx.w_arg)
             if tgt is not None:
                 _conv_wgrad(geo, x, _c(gy), alpha=alpha, out=tgt, accumulate=True)
             else:
                 gw = ConvWgrad.apply(x, gy, geo, alpha)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if ctx.has_bias and ctx.needs_input_grad[2] and wanted(ctx.b_arg):
             tgt = flat_grad(ctx.b_arg)
             if tgt is not None:
                 row_sum_acc(gy, tgt)
@@ -407,7 +422,7 @@ class ConvDgrad(Function):
         geo, alpha = ctx.geo, ctx.alpha
         g_gy = ConvFwd.apply(ggx, w, None, geo, alpha) if ctx.needs_input_grad[0] else None
         g_w = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and wanted(ctx.w_arg):
             tgt = flat_grad(ctx.w_arg)
             if tgt is not None:
                 _conv_wgrad(geo, _c(ggx), gy, alpha=alpha, out=tgt, accumulate=True)
@@ -480,8 +495,11 @@ class PReLU(Function):
             check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(x), ptr(a), C, L, ptr(gx), ptr(tgt), 1, ptr(ws), stream()),
                   "prelu_bwd")
             return gx, None
-        gx, ga = PReLUBackward.apply(gy, x, ctx.a_arg if ctx.a_arg.is_contiguous() else a)
-        return gx, ga
+        av = ctx.a_arg if ctx.a_arg.is_contiguous() else a
+        if ctx.needs_input_grad[1] and wanted(ctx.a_arg):
+            gx, ga = PReLUBackward.apply(gy, x, av)
+            return gx, ga
+        return PReLUBackwardX.apply(gy, x, av), None
 
 
 class PReLUBackward(Function):
@@ -519,6 +537,39 @@ class PReLUBackward(Function):
             tgt.add_(g_a)          # one tiny add; the kernel has no accumulate form
             g_a = None
         return g_gy, g_x, g_a
+
+
+class PReLUBackwardX(Function):
+    """gx of PReLU alone (the slope gradient is not wanted, see ``wanted``); differentiable in
+    gy (the same op) and in the slope (prelu_bwd_bwd), its x-derivative is 0 almost everywhere."""
+
+    @staticmethod
+    def forward(ctx, gy, x, a):
+        ctx.a_arg = a
+        gy = _c(gy)
+        C, L = _rows(x)
+        gx = torch.empty_like(x)
+        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), None, 0, None, stream()), "prelu_bwd")
+        ctx.save_for_backward(gy, x, a)
+        return gx
+
+    @staticmethod
+    def backward(ctx, ggx):
+        gy, x, a = ctx.saved_tensors
+        need_gy, need_x, need_a = ctx.needs_input_grad
+        g_gy = PReLUBackwardX.apply(ggx, x, ctx.a_arg) if need_gy else None
+        g_a = None
+        if need_a and wanted(ctx.a_arg):
+            C, L = _rows(x)
+            g_a = torch.empty_like(a)
+            tgt = flat_grad(ctx.a_arg)
+            ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
+            check(LIB.ganamd_prelu_bwd_bwd(ptr(_c(ggx)), None, ptr(gy), ptr(x), ptr(a), C, L, None, None, ptr(g_a),
+                                           ptr(ws), stream()), "prelu_bwd_bwd")
+            if tgt is not None:
+                tgt.add_(g_a)
+                g_a = None
+        return g_gy, None, g_a
 
 
 def prelu(x, a):

@@ -61,10 +61,33 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """``bench.py --gpus N`` started without a launcher: run N ranks under torchrun as a CHILD
+    process (this process has not touched the GPU: no exec, no HIP init) and exit with its code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print("[bench] launching:", " ".join(cmd), file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def setup_dist(n, backend):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        raise SystemExit(f"bench.py --gpus {n} but WORLD_SIZE={world}: refusing to report a {world}-rank run as {n}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "gloo":      # every rank on cuda:0 (rehearsal of the N>1 path on one GPU)
@@ -75,7 +98,6 @@ def setup_dist(n, backend):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    assert world == n or world == 1, f"--gpus {n} but WORLD_SIZE {world}"
     return world, rank, local
 
 
@@ -198,6 +220,8 @@ def build(args, dev, rank):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     if args.batch is None:
         args.batch = CONFIGS[args.config][1]
     if args.precision is None:

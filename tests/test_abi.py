@@ -35,7 +35,8 @@ def test_library_is_gfx950():
     from gan_amd import _lib
     blob = open(_lib.SO_PATH, "rb").read()
     assert b"gfx950" in blob
-    assert _lib.version().endswith("gfx950")
+    import __graft_entry__
+    assert "gfx950" in _lib.version() and _lib.version().endswith("src:" + __graft_entry__.source_hash())
 
 
 def test_invalid_arguments_rejected():

@@ -53,3 +53,14 @@ def test_checkpoint_round_trip(tmp_path):
     assert tr.optimizer_G.flat.data.data_ptr() == flat_ptr
     assert (tr.epoch, tr.i) == (4, 2)
     assert not tr.load_generator_ckpt("missing")
+
+
+def test_pickled_module_checkpoint_is_refused_clearly(tmp_path):
+    """The reference saves pickled nn.Modules (trainunits.py:58-76); they are never unpickled here."""
+    import pytest
+    _pp, tr = _trainer(tmp_path)
+    os.makedirs(tr.ckpt_root, exist_ok=True)
+    torch.save({"generator": torch.nn.Linear(2, 2), "epoch": 1, "i": 0},
+               os.path.join(tr.ckpt_root, "old.pth"))
+    with pytest.raises(RuntimeError, match="not a state_dict checkpoint"):
+        tr.load_generator_ckpt("old")
