@@ -24,6 +24,7 @@ vp = ctypes.c_void_p
 PAD_ZERO, PAD_REPLICATE = 0, 1
 EPI_STORE, EPI_BIAS, EPI_DEMOD, EPI_ACCUM, EPI_SCALE = 0, 1, 2, 3, 4
 CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
+ACT_SIGMOID, ACT_TANH, ACT_LEAKY = 0, 1, 2
 MATH_F32, MATH_BF16 = 0, 1
 
 
@@ -79,6 +80,22 @@ _SIGS = {
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),
     "ganamd_adamw": (c_int, [vp, vp, vp, vp, c_long, vp, c_float, c_float, c_float, c_float, c_float, vp]),
     "ganamd_grouped_gemm": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp]),
+    "ganamd_prelu_tangent": (c_int, [vp, vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),
+    "ganamd_act_fwd": (c_int, [c_int, vp, c_long, c_float, vp, vp]),
+    "ganamd_act_bwd": (c_int, [c_int, vp, vp, c_long, c_float, vp, vp]),
+    "ganamd_act_adjoint": (c_int, [c_int, vp, vp, vp, vp, c_long, c_float, vp, vp]),
+    "ganamd_scale_add2": (c_int, [vp, vp, vp, vp, vp, c_long, c_long, vp, vp]),
+    "ganamd_plane_dot2": (c_int, [vp, vp, vp, vp, c_long, c_long, vp, vp]),
+    "ganamd_axpy": (c_int, [c_long, c_float, vp, vp, vp]),
+    "ganamd_bce_fwd": (c_int, [vp, vp, c_int, vp, vp]),
+    "ganamd_bce_bwd": (c_int, [vp, vp, c_int, vp, vp, vp]),
+    "ganamd_softmax_m": (c_int, [c_int, vp, c_long, vp, vp]),
+    "ganamd_softmax_m_bwd": (c_int, [c_int, vp, vp, c_long, vp, vp]),
+    "ganamd_mbstd_workspace": (c_size_t, [c_int]),
+    "ganamd_mbstd_fwd": (c_int, [vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, vp, vp]),
+    "ganamd_mbstd_bwd": (c_int, [vp, c_long, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, vp]),
+    "ganamd_mbstd_tangent": (c_int, [vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, vp]),
+    "ganamd_mbstd_adjoint": (c_int, [vp, vp, c_long, vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, vp]),
     "ganamd_image_batch_workspace": (c_size_t, [c_int, c_int, c_int]),
     "ganamd_image_batch": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, c_int, c_int, vp, vp, c_int, c_int, vp, vp,
                                    vp, vp, vp]),

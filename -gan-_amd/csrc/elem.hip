@@ -799,6 +799,18 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
   return ok(hipGetLastError());
 }
 
+int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const float* alpha, int C, long L, float* yd,
+                         float* galpha, int accumulate, void* workspace, hipStream_t st) {
+  if (!xd || !gy || !x || !alpha || !yd || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
+  const int S = splits_for(L);
+  float* part = galpha ? static_cast<float*>(workspace) : nullptr;
+  hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, xd, nullptr, gy, x, alpha, L, S, yd, nullptr,
+                     part);
+  if (galpha)
+    hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, accumulate);
+  return ok(hipGetLastError());
+}
+
 int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
                       const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t st) {
   if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;

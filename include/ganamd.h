@@ -160,6 +160,11 @@ int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C,
  *   galpha[c] = sum ggx*gy over x<=0         (may be NULL) */
 int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy, const float* x, const float* alpha,
                          int C, long L, float* ggy, float* gx, float* galpha, void* workspace, hipStream_t stream);
+/* Tangent sweep of the critic's gradient-penalty double backward (critic.py) through a PReLU:
+ *   yd = xd * (x>0 ? 1 : alpha);  galpha[c] (=|+= with accumulate) sum gy*xd over x<=0
+ * (the slope's second-order term; gy = the first backward's gradient at the PReLU output). */
+int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const float* alpha, int C, long L, float* yd,
+                         float* galpha, int accumulate, void* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Separable 2-D resampling with per-axis tap tables (ELL format, K taps per output index):
@@ -261,6 +266,67 @@ size_t ganamd_image_batch_workspace(int B, int H, int OW);
 int ganamd_image_batch(const uint8_t* src, int B, int H, int W, const uint8_t* flip, const int32_t* ix,
                        const float* wx, int KX, int OW, const int32_t* iy, const float* wy, int KY, int OH,
                        const float* mean, const float* stdv, float* y, float* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Pointwise activations (csrc/act.hip) over n contiguous floats.
+ *   GANAMD_ACT_SIGMOID  SE gates (generator_13_5.py:357,376; discriminator_9_4.py:109,128),
+ *                       the vanilla critic's Sigmoid (discriminator_1.py:20)
+ *   GANAMD_ACT_TANH     the vanilla generator's Tanh (generator_1.py:23)
+ *   GANAMD_ACT_LEAKY    LeakyReLU(slope) (generator_1.py:19,21; discriminator_1.py:16,18)
+ * ganamd_act_bwd: gx = gy * f'(.) where v is the forward OUTPUT for sigmoid / tanh and the
+ * forward INPUT for leaky.
+ * ------------------------------------------------------------------------------------- */
+#define GANAMD_ACT_SIGMOID 0
+#define GANAMD_ACT_TANH 1
+#define GANAMD_ACT_LEAKY 2
+int ganamd_act_fwd(int kind, const float* x, long n, float slope, float* y, hipStream_t stream);
+int ganamd_act_bwd(int kind, const float* v, const float* gy, long n, float slope, float* gx, hipStream_t stream);
+/* Adjoint sweep of the critic's gradient-penalty double backward (critic.py) through an
+ * activation: ax = ay * f'(.) + gy * xd * f''(.)  (v as for ganamd_act_bwd; f'' = 0 for leaky). */
+int ganamd_act_adjoint(int kind, const float* v, const float* ay, const float* gy, const float* xd, long n, float slope,
+                       float* ax, hipStream_t stream);
+
+/* y = x1 * s1[plane] + x2 * s2[plane] + r over planes of HW floats (x2/s2 and r may be NULL): the
+ * tangent and adjoint of the SE-gated residual y = x * s + r (discriminator_9_4.py:158-161). */
+int ganamd_scale_add2(const float* x1, const float* s1, const float* x2, const float* s2, const float* r, long planes,
+                      long HW, float* y, hipStream_t stream);
+/* out[plane] = sum a1*b1 + sum a2*b2 (a2/b2 may be NULL): the gate's adjoint of the same op. */
+int ganamd_plane_dot2(const float* a1, const float* b1, const float* a2, const float* b2, long planes, long HW,
+                      float* out, hipStream_t stream);
+/* y += a * x over n floats (gradient accumulation where an activation feeds two consumers). */
+int ganamd_axpy(long n, float a, const float* x, float* y, hipStream_t stream);
+
+/* torch.nn.BCELoss (mean; logs clamped at -100) of probabilities p against targets, n values
+ * (train/gan.py:21,32,48,50).  out: device scalar.  ganamd_bce_bwd: gp = d out/d p * gout[0]. */
+int ganamd_bce_fwd(const float* p, const float* target, int n, float* out, hipStream_t stream);
+int ganamd_bce_bwd(const float* p, const float* target, int n, const float* gout, float* gp, hipStream_t stream);
+
+/* Softmax over M in {2,3,4} branches of x[M][P] (the SK attention heads, dim=1 of the
+ * reference's [B, M, C, 1, 1]: generator_13_5.py:88,131) and its backward gx = y (gy - <y, gy>). */
+int ganamd_softmax_m(int M, const float* x, long P, float* y, hipStream_t stream);
+int ganamd_softmax_m_bwd(int M, const float* y, const float* gy, long P, float* gx, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * MiniBatchStdDev (discriminator_9_4.py:42-54) on CNHW x[C][B][HW] (row stride ldx floats)
+ * holding S independent segments of B/S samples; group size G = 4 (x.view(G, -1) of each
+ * segment's NCHW tensor, unbiased variance, + 1e-8, sqrt, mean).  y[C+1][B][HW] (row stride
+ * ldy) = x with one more row holding each segment's std; std_out[S] (may be NULL).
+ *   bwd      gx = d/dx <gy, y>
+ *   tangent  yd = directional derivative of y along xd (the forward sweep of the critic's
+ *            gradient-penalty double backward, critic.py)
+ *   adjoint  ax = J^T ay + (d(J xd)/dx)^T gy (its reverse sweep: the second-order term of the
+ *            batch coupling)
+ * Workspace: ganamd_mbstd_workspace(S) bytes.
+ * ------------------------------------------------------------------------------------- */
+size_t ganamd_mbstd_workspace(int S);
+int ganamd_mbstd_fwd(const float* x, long ldx, int C, int B, int HW, int S, int G, float* y, long ldy, float* std_out,
+                     void* workspace, hipStream_t stream);
+int ganamd_mbstd_bwd(const float* x, long ldx, const float* gy, long ldy, int C, int B, int HW, int S, int G,
+                     float* gx, void* workspace, hipStream_t stream);
+int ganamd_mbstd_tangent(const float* x, const float* xd, long ldx, int C, int B, int HW, int S, int G, float* yd,
+                         long ldy, void* workspace, hipStream_t stream);
+int ganamd_mbstd_adjoint(const float* x, const float* xd, long ldx, const float* gy, const float* ay, long ldy, int C,
+                         int B, int HW, int S, int G, float* ax, void* workspace, hipStream_t stream);
 
 /* Library identification (for load checks). */
 const char* ganamd_version(void);
