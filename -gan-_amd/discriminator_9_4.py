@@ -7,9 +7,11 @@ gradient penalty of train/wgangp.py:34-54): every operator used here is closed u
 differentiation (see ops.py).
 
 Underneath: CNHW activations, MFMA implicit-GEMM convs (replication padding folded into the
-gather, stride 2 included), PReLU kernels with first/second derivatives, and Smooth /
+gather, stride 2 included), PReLU kernels with first/second derivatives, Smooth /
 bicubic-downsample / adaptive-pool as tap-table resamples (DownSample's smooth+bicubic is one
-composed table).
+composed table), MiniBatchStdDev and the SE sigmoid as kernels.  ``forward`` runs the layer
+program of critic.py (explicit backward and gradient-penalty double backward);
+``forward_autograd`` keeps the per-layer autograd formulation for A/B tests.
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ from typing import List
 import torch
 from torch import nn
 
-from . import ops
+from . import critic, ops
 from .ops import prelu
 
 
@@ -203,7 +205,16 @@ class Discriminator(nn.Module):
         """``segments`` > 1: ``input`` is that many independent mini-batches stacked along the
         batch (the critic step runs its real and fake batches as one pass); every layer is
         per-sample except MiniBatchStdDev, which is computed per segment, so the output equals
-        the per-segment calls concatenated."""
+        the per-segment calls concatenated.
+
+        Runs the critic as the explicit layer program of critic.py: one autograd node whose
+        backward (and, under create_graph, double backward) are kernel sweeps over the saved
+        activations -- no per-layer autograd graph."""
+        return critic.critic_forward(self, input, segments)
+
+    def forward_autograd(self, input, segments: int = 1):
+        """The same forward as per-layer autograd Functions (ops.py), every one of them closed
+        under differentiation: the A/B reference for the explicit program in the GPU tests."""
         B = input.shape[0]
         for mod in self.conv:
             if isinstance(mod, MiniBatchStdDev):

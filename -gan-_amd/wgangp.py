@@ -23,8 +23,9 @@ import contextlib
 
 import torch
 
-from . import ops
+from . import critic, ops
 from .checkpoint import CheckpointMixin
+from .discriminator_9_4 import Discriminator
 from .optim import FusedAdamW
 from .rng import DeviceRNG
 
@@ -94,13 +95,16 @@ class Train(CheckpointMixin):
         """train/wgangp.py:34-43."""
         eps = self.rng.rand((batch_size,)).view(batch_size, 1, 1, 1)
         x_interp = ((1 - eps) * x_real + eps * x_fake).detach()
-        x_interp.requires_grad_()
-        d_out = self.discriminator(x_interp)
-        # (compute_grad2(d_out, x_interp).sqrt() - center).pow(2).mean(), with the norm, the
-        # penalty and its gradient in two fused kernels (ops.GradPenalty)
-        grad = torch.autograd.grad(outputs=d_out.sum(), inputs=x_interp, create_graph=True, retain_graph=True,
-                                   only_inputs=True)[0]
-        return ops.grad_penalty(grad, center, 1.0, 0)
+        if not isinstance(self.discriminator, Discriminator):     # e.g. the progan critic
+            x_interp.requires_grad_()
+            d_out = self.discriminator(x_interp)
+            grad = torch.autograd.grad(outputs=d_out.sum(), inputs=x_interp, create_graph=True, retain_graph=True,
+                                       only_inputs=True)[0]
+            return ops.grad_penalty(grad, center, 1.0, 0)
+        # (compute_grad2(d_out, x_interp).sqrt() - center).pow(2).mean() as the critic program of
+        # critic.py: forward, input-gradient sweep and the fused penalty now; the returned value's
+        # backward() runs the double backward as two explicit sweeps (no autograd graph of D)
+        return critic.gradient_penalty(self.discriminator, x_interp, center, 1.0, 0)
 
     def compute_grad2(self, d_out, x_in):
         """train/wgangp.py:45-54."""

@@ -25,7 +25,8 @@ from __future__ import annotations
 
 import torch
 
-from . import ops, wgangp
+from . import critic, ops, wgangp
+from .discriminator_9_4 import Discriminator
 from .optim import FusedAdamW
 
 LAZY_INTERVAL = 5      # wganlazygpR2.py:56,65,71: regularisers every 5th critic step
@@ -78,6 +79,19 @@ class Train(wgangp.Train):
             return real_loss, fake_loss, zero, zero.clone(), zero.clone()
         eps = self.rng.rand((b_size,)).view(b_size, 1, 1, 1)
         x_interp = (1 - eps) * images + eps * gen_imgs
+        if isinstance(self.discriminator, Discriminator):
+            # one pass of each sweep of the critic program (critic.py) over the three segments:
+            # loss weights -1/B (real), +1/B (fake), 0 (interpolated) folded into the adjoint seed
+            x = torch.cat([images, gen_imgs, x_interp]).detach()
+            w = torch.cat([torch.full((b_size,), -1.0 / b_size, device=x.device),
+                           torch.full((b_size,), 1.0 / b_size, device=x.device),
+                           torch.zeros(b_size, device=x.device)])
+            pred, (r2_reg_r, r2_reg_f, gp) = critic.regularised_step(
+                self.discriminator, x, 3, w,
+                [(0.0, float(REG_WEIGHT), 1), (0.0, float(REG_WEIGHT), 1), (1.0, float(GP_LAMBDA * REG_WEIGHT), 0)])
+            real_loss = -torch.mean(pred[:b_size])
+            fake_loss = torch.mean(pred[b_size:2 * b_size])
+            return real_loss, fake_loss, gp, r2_reg_r, r2_reg_f
         x = torch.cat([images, gen_imgs, x_interp]).detach().requires_grad_()
         pred = self.discriminator(x, segments=3)
         grad = torch.autograd.grad(pred.sum(), x, create_graph=True, retain_graph=True, only_inputs=True)[0]

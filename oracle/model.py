@@ -67,10 +67,23 @@ class Params:
 # shared primitives
 # ----------------------------------------------------------------------------------------------
 
+# bf16 emulation of the build's GANAMD_MATH_BF16 GEMMs (test infrastructure for config 4, which
+# the reference does not have): when set, the two GEMM operands of every equalized conv / linear
+# -- the (padded) input and the UNSCALED weight -- are rounded to bf16 (RNE) before the product;
+# the equalized-LR scale and the bias apply after it, in the working precision.
+BF16_GEMM = [False]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(t.dtype) if BF16_GEMM[0] else t
+
+
 def eq_linear(P, pre, x, cin, cout, wname="weights", bias_init="randn"):
     """EqualizedLinear: generator_13_5.py:19-26 / discriminator_9_4.py:20-27."""
     w = P(f"{pre}.weight.{wname}", (cout, cin))
     b = P(f"{pre}.bias", (cout,), bias_init)
+    if BF16_GEMM[0]:
+        return F.linear(_bf(x), _bf(w)) * (1.0 / math.sqrt(cin)) + b
     return F.linear(x, w * (1.0 / math.sqrt(cin)), b)
 
 
@@ -80,6 +93,8 @@ def eq_conv(P, pre, x, cin, cout, k, pad, stride=1, wname="weights"):
     b = P(f"{pre}.bias", (cout,))
     if pad:
         x = F.pad(x, (pad, pad, pad, pad), mode="replicate")
+    if BF16_GEMM[0]:
+        return F.conv2d(_bf(x), _bf(w), None, stride=stride) * (1.0 / math.sqrt(cin * k * k)) + b.view(1, -1, 1, 1)
     return F.conv2d(x, w * (1.0 / math.sqrt(cin * k * k)), b, stride=stride)
 
 
@@ -102,7 +117,7 @@ def smooth(x):
     """Smooth: depthwise binomial 3x3 with replication pad (generator_13_5.py:134-150)."""
     b, c, h, w = x.shape
     y = F.pad(x.reshape(b * c, 1, h, w), (1, 1, 1, 1), mode="replicate")
-    return F.conv2d(y, _SMOOTH.view(1, 1, 3, 3)).reshape(b, c, h, w)
+    return F.conv2d(y, _SMOOTH.to(x.dtype).view(1, 1, 3, 3)).reshape(b, c, h, w)
 
 
 def softmax_mix(feas, att):
