@@ -53,7 +53,10 @@ constexpr int LDK = BK + 4;
 #else
 constexpr int LDK = BK + 2;   // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
 #endif
-constexpr int BKW = 32;       // wgrad K-step (pixels): a half-wave reads one full 128-byte line
+#ifndef GANAMD_BKW
+#define GANAMD_BKW 32
+#endif
+constexpr int BKW = GANAMD_BKW; // wgrad K-step (pixels): at 32 a half-wave reads one full 128-byte line
 constexpr int LDKW = BKW + 2;
 
 enum GatherMode { kZero = 0, kReplicate = 1, kTransposed = 2 };
@@ -272,8 +275,15 @@ __global__ void pack_a_kernel(const float* __restrict__ w, int sm, int sc, int s
   }
 }
 
+#ifndef GANAMD_CONV_WPE
+#define GANAMD_CONV_WPE 1
+#endif
+#ifndef GANAMD_WGRAD_WPE
+#define GANAMD_WGRAD_WPE 1
+#endif
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
-__global__ __launch_bounds__(kThreads) void conv_gemm_kernel(ConvArgs p) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD_CONV_WPE)))
+void conv_gemm_kernel(ConvArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int A4 = BM * BK / 4;                      // 16-byte slots of the A tile
   constexpr int EA = (A4 + kThreads - 1) / kThreads;   // slots per thread
@@ -476,7 +486,8 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
 // wgrad: K = output pixels n, M = output channels of the conv, N = gathered channels at tap t
 // ------------------------------------------------------------------------------------------
 template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED, bool BF16>
-__global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD_WGRAD_WPE)))
+void wgrad_gemm_kernel(WgradArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int A4 = BM * BKW / 4;                     // 16-byte slots of the A tile (4 pixels of a row)
   constexpr int EA = (A4 + kThreads - 1) / kThreads;
@@ -531,7 +542,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
     for (int e = 0; e < EA; ++e) {
       const int slot = tid + e * kThreads;
       if (slot < A4) {
-        const int m = m0 + (slot >> 3), n = kt * BKW + 4 * (slot & 7);
+        const int m = m0 + slot / (BKW / 4), n = kt * BKW + 4 * (slot % (BKW / 4));
         const bool mok = m < p.M;
         if (full) {
           ra[e] = bload4(ra_r, mok ? 4 * (m * p.lda + n) : kOOB);
@@ -583,7 +594,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
       if (slot < A4) {
         f32x4 v = ra[e];
         if (SCALED) v *= rsa[e];
-        float* d = &As[buf][(slot >> 3) * LDKW + 4 * (slot & 7)];
+        float* d = &As[buf][(slot / (BKW / 4)) * LDKW + 4 * (slot % (BKW / 4))];
         *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
         *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
       }
@@ -602,8 +613,8 @@ __global__ __launch_bounds__(kThreads) void wgrad_gemm_kernel(WgradArgs p) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
-    mfma_tile<C, LDKW, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, 0);
-    mfma_tile<C, LDKW, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, 16);
+#pragma unroll
+    for (int k0 = 0; k0 < BKW; k0 += 16) mfma_tile<C, LDKW, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
@@ -922,6 +933,29 @@ size_t pack_bytes(int M, int Ck, int T) {
   return sizeof(float) * mpad * T * (size_t)((Ck + BK - 1) / BK * BK);
 }
 
+template <int BM, int BN, int WGM, int WGN, bool SCALED>
+int wgrad_occ() {
+  static const int v = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wgrad_gemm_kernel<BM, BN, WGM, WGN, kReplicate, SCALED, false>,
+                                                     kThreads, 0) != hipSuccess || n <= 0)
+      n = 2;
+    return n;
+  }();
+  return v;
+}
+
+template <bool SCALED>
+int wgrad_occ_tile(int bm, int bn) {
+  if (bn == 64) return wgrad_occ<64, 64, 2, 2, SCALED>();
+  switch (bm) {
+    case 32: return wgrad_occ<32, 128, 1, 4, SCALED>();
+    case 64: return wgrad_occ<64, 128, 2, 2, SCALED>();
+    case 96: return wgrad_occ<96, 128, 1, 4, SCALED>();
+    default: return wgrad_occ<128, 128, 2, 2, SCALED>();
+  }
+}
+
 Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
   int bm = wgrad_bm(M, scaled), bn = 128;
   if (J <= 64 && bm >= 64) {  // narrow gathered side: a 64x64 tile wastes nothing on J = 48..64
@@ -929,7 +963,7 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
     bn = 64;
   }
   const int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
-  const int occ = bn == 64 ? 4 : (bm >= 96 ? 2 : 3);
+  const int occ = scaled ? wgrad_occ_tile<true>(bm, bn) : wgrad_occ_tile<false>(bm, bn);
   return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, 2.0 * bm * bn * BKW, (long)M * J * T, occ, 256, 4);
 }
 

@@ -990,3 +990,70 @@ def nchw_to_cnhw(x):
 
 def cnhw_to_nchw(x):
     return _SwapNC.apply(x)
+
+
+# ------------------------------------------------------------------------------------------
+# pointwise activations and BCE (the vanilla pair of config 1: generator_1.py, discriminator_1.py,
+# train/gan.py)
+# ------------------------------------------------------------------------------------------
+
+
+class Act(Function):
+    """Sigmoid / Tanh / LeakyReLU(slope) over a contiguous tensor (csrc/act.hip).  The backward
+    reads the forward OUTPUT for sigmoid / tanh and the forward INPUT for leaky."""
+
+    @staticmethod
+    def forward(ctx, x, kind, slope):
+        x = _c(x)
+        y = torch.empty_like(x)
+        check(LIB.ganamd_act_fwd(int(kind), ptr(x), x.numel(), float(slope), ptr(y), stream()), "act_fwd")
+        ctx.save_for_backward(x if kind == _lib.ACT_LEAKY else y)
+        ctx.kind, ctx.slope = int(kind), float(slope)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (v,) = ctx.saved_tensors
+        gy = _c(gy)
+        gx = torch.empty_like(v)
+        check(LIB.ganamd_act_bwd(ctx.kind, ptr(v), ptr(gy), v.numel(), ctx.slope, ptr(gx), stream()), "act_bwd")
+        return gx, None, None
+
+
+def sigmoid(x):
+    return Act.apply(x, _lib.ACT_SIGMOID, 0.0)
+
+
+def tanh(x):
+    return Act.apply(x, _lib.ACT_TANH, 0.0)
+
+
+def leaky_relu(x, slope):
+    return Act.apply(x, _lib.ACT_LEAKY, slope)
+
+
+class BCELoss(Function):
+    """torch.nn.BCELoss() (mean reduction, logs clamped at -100) of probabilities p against
+    targets (train/gan.py:21); the gradient reaches p only (targets are constants there)."""
+
+    @staticmethod
+    def forward(ctx, p, target):
+        p, target = _c(p), _c(target)
+        if p.shape != target.shape:
+            raise ValueError(f"BCELoss: input {tuple(p.shape)} vs target {tuple(target.shape)}")
+        out = torch.empty((), device=p.device, dtype=torch.float32)
+        check(LIB.ganamd_bce_fwd(ptr(p), ptr(target), p.numel(), ptr(out), stream()), "bce_fwd")
+        ctx.save_for_backward(p, target)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        p, target = ctx.saved_tensors
+        gout = _c(gout.reshape(1))
+        gp = torch.empty_like(p)
+        check(LIB.ganamd_bce_bwd(ptr(p), ptr(target), p.numel(), ptr(gout), ptr(gp), stream()), "bce_bwd")
+        return gp, None
+
+
+def bce_loss(p, target):
+    return BCELoss.apply(p, target)

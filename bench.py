@@ -17,7 +17,8 @@ Also reported (rank 0):
                 over the measured iteration time, against the fp32 MFMA peak (157.3 TFLOP/s);
                 plus the conv-GEMM FLOPs this build actually issues per iteration.
   cpu_baseline  the CPU oracle (oracle/model.py, fp32 PyTorch-CPU restatement pinned to the
-                reference's golden fixtures) timed on the host: 1 D-step + 1 G-step at B=4.
+                reference's golden fixtures) timed on the host at B=8: one
+                warm-up D-step + G-step, then 2 timed D-steps + 1 timed G-step.
 """
 from __future__ import annotations
 
@@ -101,28 +102,46 @@ def setup_dist(n, backend):
     return world, rank, local
 
 
-def cpu_baseline(threads):
-    """Time the CPU oracle: 1 D-step + 1 G-step at B=4 -> images/sec of a full iteration."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(threads, B=8):
+    """Time the CPU oracle: B=8, one warm-up D-step + G-step (untimed), then two
+    timed D-steps and one timed G-step -> t_iter = 5 * mean(t_D) + t_G -> images/sec."""
     from oracle import model as om
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     GP, DP = om.Params(lazy=True, generator=g), om.Params(lazy=True, generator=g)
     draw = om.Draw(1)
     with torch.no_grad():  # materialise every parameter once (lazy init) outside the timing
-        om.generator(GP, torch.randn(4, 256, 1, 1), draw.randn)
-        om.discriminator(DP, torch.randn(4, 3, 64, 64))
+        om.generator(GP, torch.randn(B, 256, 1, 1), draw.randn)
+        om.discriminator(DP, torch.randn(B, 3, 64, 64))
     tr = om.WGANGP(GP, DP)
-    B = 4
-    imgs = torch.randn(B, 3, 64, 64, generator=g)
-    t0 = time.perf_counter()
-    tr.discriminator_trainstep(imgs, B, draw)
-    t1 = time.perf_counter()
+    tr.discriminator_trainstep(torch.randn(B, 3, 64, 64, generator=g), B, draw)     # warm-up
     tr.generator_trainstep(B, draw)
-    t2 = time.perf_counter()
-    t_iter = N_CRITIC * (t1 - t0) + (t2 - t1)
+    t_d = []
+    for _ in range(2):
+        imgs = torch.randn(B, 3, 64, 64, generator=g)
+        t0 = time.perf_counter()
+        tr.discriminator_trainstep(imgs, B, draw)
+        t_d.append(time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    tr.generator_trainstep(B, draw)
+    t_g = time.perf_counter() - t0
+    t_iter = N_CRITIC * sum(t_d) / len(t_d) + t_g
     return {"value": B / t_iter, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"CPU oracle (fp32 PyTorch-CPU restatement), B=4: 1 D-step {t1 - t0:.2f}s + 1 G-step "
-                      f"{t2 - t1:.2f}s, t_iter = 5*t_D + t_G = {t_iter:.1f}s; nproc={os.cpu_count()}"}
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"CPU oracle (fp32 PyTorch-CPU restatement of the reference step), B={B}: 1 warm-up D-step + "
+                      f"G-step, then D-steps {', '.join(f'{t:.2f}s' for t in t_d)} and G-step {t_g:.2f}s timed; "
+                      f"t_iter = 5*mean(t_D) + t_G = {t_iter:.1f}s"}
 
 
 # Dominant kernel: the implicit-GEMM conv kernel (conv_gemm_kernel, all instances ~55-65 % of the

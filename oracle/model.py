@@ -607,6 +607,71 @@ class WGANLazyR2(WGANGP):
         return real_loss, fake_loss, gp, r1, r2
 
 
+# ----------------------------------------------------------------------------------------------
+# Vanilla pair + BCE trainer (config 1: generators/generator_1.py, discriminators/discriminator_1.py,
+# train/gan.py)
+# ----------------------------------------------------------------------------------------------
+
+def vanilla_generator(P, z, randn=None, image=(3, 64, 64)):
+    """generator_1.py:16-29: Linear z->256, LeakyReLU(0.2), Linear 256->512, LeakyReLU(0.2),
+    Linear 512->3*64*64, Tanh, viewed as [B, 3, 64, 64]."""
+    x = z.reshape(z.shape[0], -1)
+    dims = [x.shape[1], 256, 512, image[0] * image[1] * image[2]]
+    for j, i in enumerate((0, 2, 4)):
+        x = F.linear(x, P(f"generator.{i}.weight", (dims[j + 1], dims[j])), P(f"generator.{i}.bias", (dims[j + 1],)))
+        x = F.leaky_relu(x, 0.2) if i < 4 else torch.tanh(x)
+    return x.view(z.shape[0], *image)
+
+
+def vanilla_discriminator(P, x):
+    """discriminator_1.py:14-25: Linear 12288->256, LeakyReLU(0.2), Linear 256->64, LeakyReLU(0.2),
+    Linear 64->1, Sigmoid."""
+    h = x.reshape(x.shape[0], -1)
+    dims = [h.shape[1], 256, 64, 1]
+    for j, i in enumerate((0, 2, 4)):
+        h = F.linear(h, P(f"discriminator.{i}.weight", (dims[j + 1], dims[j])),
+                     P(f"discriminator.{i}.bias", (dims[j + 1],)))
+        h = F.leaky_relu(h, 0.2) if i < 4 else torch.sigmoid(h)
+    return h
+
+
+class GAN(WGANGP):
+    """The oracle counterpart of ``train/gan.py:Train`` (BCE with noisy labels) with the Adam
+    optimizers of ``train/trainunits.py:18-19``."""
+
+    def __init__(self, GP: Params, DP: Params, nz=256):
+        super().__init__(GP, DP, nz, vanilla_generator, vanilla_discriminator)
+        self.opt_G = torch.optim.Adam([GP.t[k] for k in self.g_order], lr=1e-4, betas=(0.5, 0.99))
+        self.opt_D = torch.optim.Adam([DP.t[k] for k in self.d_order], lr=4e-4, betas=(0.0, 0.99))
+
+    def generator_trainstep(self, b, draw):
+        """gan.py:26-35: targets 0.95 + 0.05 U[0,1)."""
+        valid = 0.95 + 0.05 * draw.rand((b, 1))
+        self.opt_G.zero_grad()
+        z = draw.randn((b, self.nz, 1, 1))
+        gen = self.gen(self.GP, z)
+        g_loss = F.binary_cross_entropy(self.disc(self.DP, gen), valid)
+        g_loss.backward()
+        self.opt_G.step()
+        return gen, g_loss
+
+    def discriminator_trainstep(self, images, b, draw):
+        """gan.py:37-53: real targets 0.95 + 0.05 U, fake targets 0.05 U (drawn in that order),
+        then z."""
+        valid = 0.95 + 0.05 * draw.rand((b, 1))
+        fake = 0.0 + 0.05 * draw.rand((b, 1))
+        z = draw.randn((b, self.nz, 1, 1))
+        self.opt_D.zero_grad()
+        with torch.no_grad():
+            gen = self.gen(self.GP, z)
+        real_loss = F.binary_cross_entropy(self.disc(self.DP, images), valid)
+        real_loss.backward()
+        fake_loss = F.binary_cross_entropy(self.disc(self.DP, gen), fake)
+        fake_loss.backward()
+        self.opt_D.step()
+        return real_loss, fake_loss
+
+
 class Draw:
     """Randomness replayed from one CPU generator in call order (the reference's global-RNG order)."""
 

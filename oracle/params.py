@@ -34,6 +34,8 @@ _KIND = {
     ("Smooth", "kernel"): "smooth",             # frozen binomial kernel, requires_grad=False
     ("Conv2d", "weight"): "eqw",                # progan D: nn.Conv2d inside EqualizedConv2d, N(0,1) init
                                                 # (discriminator_3_wgangp_progan.py:20-24)
+    ("Linear", "weight"): "lin_w",              # vanilla pair: plain nn.Linear (generator_1.py:18-22,
+    ("Linear", "bias"): "lin_b",                # discriminator_1.py:15-19)
 }
 
 
@@ -78,6 +80,10 @@ def fill_value(seed: int, index: int, kind: str, shape) -> torch.Tensor | None:
         return 0.25 + 0.02 * n
     if kind == "style_bias":
         return n
+    if kind == "lin_w":      # N(0, 1/fan_in): keeps the vanilla critic's sigmoid out of saturation
+        return n / math.sqrt(shape[1])
+    if kind == "lin_b":
+        return 0.1 * n
     raise KeyError(kind)
 
 

@@ -335,3 +335,43 @@ def test_lazy_bf16_steps(gan, P):
         images = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(600)).to(DEV)
         out.append([float(v.detach().reshape(-1)[0]) for v in tr.discriminator_trainstep(images, 4, 0)])
     assert out[0] == out[1], out
+
+
+def test_critic_b64(gan, P):
+    """The headline batch (B=64, config 2) against the reference's own critic run at B=64
+    (tests/golden/make_golden_b64.py): critic output, per-sample input-gradient norms and sampled
+    input-gradient elements.  Exercises the B=64 launch schedules (split-K tails, scatter dgrad of
+    the strided convs) the bench runs."""
+    from oracle.params import summary_indices
+    fx = fixture("d_step_b64.npz")
+    D = make_D(gan, P)
+    x = torch.randn(64, 3, 64, 64, generator=torch.Generator().manual_seed(320)).to(DEV).requires_grad_()
+    out = D(x)
+    gx, = torch.autograd.grad(out.sum(), x)
+    torch.cuda.synchronize()
+    assert rel_err(out.detach().cpu().numpy(), fx["d_out"]) < 1e-4
+    assert rel_err(gx.reshape(64, -1).norm(dim=1).cpu().numpy(), fx["gx_norm"]) < 1e-4
+    idx = torch.as_tensor(summary_indices(gx.numel(), 64))
+    assert rel_err(gx.reshape(-1)[idx.to(DEV)].cpu().numpy(), fx["gx_samples"]) < 1e-3
+
+
+def test_d_step_b64(gan, P):
+    """One full WGAN-GP critic step at B=64 (generator forward, critic on real and fake, gradient
+    penalty with its double backward, AdamW) against the reference's run of the same step: losses
+    at 1e-4 and the step gradients by the norm-based bars the CPU oracle meets at B=4/8 (D_BAR)."""
+    from tests._util import D_BAR, check_grads
+    fx = fixture("d_step_b64.npz")
+    G, D = make_G(gan, P), make_D(gan, P)
+    tr = gan.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(331, DEV))
+    images = torch.randn(64, 3, 64, 64, generator=torch.Generator().manual_seed(330)).to(DEV)
+    names = [n for n, _, _ in P["d_params"]]
+    before = {n: p.detach().clone() for n, p in D.named_parameters()}
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, 64)]
+    assert rel_err(losses, fx["losses"]) < 1e-4, (losses, fx["losses"])
+    rows = _rows(D, names)
+    has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
+    assert (has == fx["has_grad"]).all()
+    check_grads(rows, fx["grads"], D_BAR)
+    params = dict(D.named_parameters())
+    dl = np.asarray([tensor_summary((params[n].detach() - before[n]) / 4e-4)[1] for n in names])
+    assert rel_err(dl, fx["deltas"][:, 1]) < 2e-3

@@ -5,7 +5,7 @@ import torch
 
 from oracle import model as om
 from oracle.params import tensor_summary
-from tests._util import D_BAR, G_BAR, check_grads, fixture, plan, rel_err
+from tests._util import D_BAR, G_BAR, check_grads, fixture, plan, rel_err, summary_check
 
 @pytest.fixture(scope="module")
 def P():
@@ -238,3 +238,64 @@ def test_progan_steps():
     assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-4
     rows, _ = _step_rows(GP, [n for n, _, _ in pp["g_params"]])
     check_grads(rows, fx["g_grads"], G_BAR)
+
+
+# ---- vanilla pair + BCE trainer (config 1; tests/golden/make_golden_gan.py) ------------------
+
+def _gan():
+    import json
+    import os
+    from tests._util import GOLDEN
+    with open(os.path.join(GOLDEN, "plan_gan.json")) as f:
+        pp = json.load(f)
+    return pp, om.params_from_plan(pp["g_params"], pp["g_seed"]), om.params_from_plan(pp["d_params"], pp["d_seed"])
+
+
+def test_gan_forward():
+    """generator_1.py / discriminator_1.py restated: outputs at 1e-6 of the reference's."""
+    fx = fixture("gan_b16.npz")
+    pp, GP, DP = _gan()
+    x = torch.randn(16, 3, 64, 64, generator=torch.Generator().manual_seed(int(fx["d_fwd_x_seed"][0])))
+    with torch.no_grad():
+        assert rel_err(om.vanilla_generator(GP, torch.from_numpy(fx["g_fwd_z"])), fx["g_fwd_out"]) < 1e-6
+        assert rel_err(om.vanilla_discriminator(DP, x), fx["d_fwd_out"]) < 1e-6
+    assert GP.used == {n for n, _, _ in pp["g_params"]} and DP.used == {n for n, _, _ in pp["d_params"]}
+
+
+def test_gan_steps():
+    """train/gan.py:26-53 (BCE, noisy labels, Adam of trainunits.py:18-19) at B=16: losses,
+    every gradient summary and every Adam update against the reference's fixture."""
+    fx = fixture("gan_b16.npz")
+    pp, GP, DP = _gan()
+    tr = om.GAN(GP, DP)
+    images = torch.randn(16, 3, 64, 64, generator=torch.Generator().manual_seed(710))
+    before = {k: v.detach().clone() for k, v in DP.t.items()}
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, 16, om.Draw(711))]
+    assert rel_err(losses, fx["d_losses"]) < 1e-6
+    rows, dl = _step_rows(DP, [n for n, _, _ in pp["d_params"]], before, 4e-4)
+    assert summary_check(rows, fx["d_grads"])[0] < 1e-4
+    assert rel_err(dl, fx["d_deltas"][:, 1]) < 1e-4
+    pp, GP, DP = _gan()
+    tr = om.GAN(GP, DP)
+    before = {k: v.detach().clone() for k, v in GP.t.items()}
+    gen, g_loss = tr.generator_trainstep(16, om.Draw(721))
+    assert rel_err([float(g_loss)], fx["g_loss"]) < 1e-6
+    assert rel_err(tensor_summary(gen), fx["g_gen"]) < 1e-6
+    rows, dl = _step_rows(GP, [n for n, _, _ in pp["g_params"]], before, 1e-4)
+    assert summary_check(rows, fx["g_grads"])[0] < 1e-4
+    assert rel_err(dl, fx["g_deltas"][:, 1]) < 1e-4
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not __import__("os").environ.get("GANAMD_SLOW"), reason="~2 min of CPU: set GANAMD_SLOW=1")
+def test_d_step_b64(P):
+    """The oracle's critic step at the headline batch against the reference's (make_golden_b64.py):
+    the same bars the GPU path is held to in tests/test_models_gpu.py::test_d_step_b64."""
+    fx = fixture("d_step_b64.npz")
+    GP, DP = _g(P), _d(P)
+    tr = om.WGANGP(GP, DP)
+    images = torch.randn(64, 3, 64, 64, generator=torch.Generator().manual_seed(330))
+    losses = [float(v.detach()) for v in tr.discriminator_trainstep(images, 64, om.Draw(331))]
+    assert rel_err(losses, fx["losses"]) < 1e-4
+    rows, _ = _step_rows(DP, [n for n, k, _ in P["d_params"]])
+    check_grads(rows, fx["grads"], D_BAR)

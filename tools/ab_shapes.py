@@ -1,0 +1,78 @@
+"""A/B timing of the iteration's dominant GEMM shapes across library builds.
+
+    python tools/ab_shapes.py LIB1.so [LIB2.so ...]      (each build in its own child process)
+
+Shapes: the largest GEMMs of one WGAN-GP iteration at B=64 (profiles/*census*): generator
+modulated convs (scaled), critic block convs on the 2B = 128 real+fake batch, their dgrad / wgrad,
+the strided scatter dgrad and the 4x4 1025-channel block.  Prints us and TF/s per shape and the
+count-weighted total."""
+import os
+import subprocess
+import sys
+
+SHAPES = [  # (op, B, cin, H, cout, k, stride, pad, scaled, weight = launches per iteration)
+    ("fwd", 64, 96, 64, 96, 5, 1, 2, True, 60),
+    ("fwd", 64, 48, 64, 48, 5, 1, 2, True, 120),
+    ("fwd", 64, 48, 64, 48, 3, 1, 1, True, 180),
+    ("fwd", 128, 128, 32, 128, 3, 1, 1, False, 25),
+    ("fwd", 64, 192, 16, 192, 5, 1, 2, True, 60),
+    ("wgrad", 128, 128, 32, 128, 3, 1, 1, False, 25),
+    ("wgrad", 64, 96, 64, 96, 5, 1, 2, True, 10),
+    ("wgrad", 64, 1025, 4, 1025, 3, 1, 1, False, 90),
+    ("wgrad", 128, 64, 64, 64, 3, 1, 1, False, 25),
+    ("dgrad", 128, 64, 64, 64, 3, 1, 1, False, 25),
+    ("dgrad", 64, 96, 64, 96, 5, 1, 2, True, 10),
+    ("dgrad", 64, 1024, 8, 1024, 3, 2, 1, False, 11),
+    ("dgrad", 64, 1025, 4, 1025, 3, 1, 1, False, 66),
+]
+
+
+def child():
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from gan_amd import ops
+    dev = torch.device("cuda")
+    tot_t = tot_f = 0.0
+    for op, B, cin, H, cout, k, s, p, scaled, n in SHAPES:
+        g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
+        x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
+        y = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
+        w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
+        sx = torch.rand(g.Cin, g.B, device=dev) if scaled else None
+        sy = torch.rand(g.Cout, g.B, device=dev) if scaled else None
+        f = {"fwd": lambda: ops._conv_fwd(g, x, w, None, sx, sy, 1.0),
+             "dgrad": lambda: ops._conv_dgrad(g, y, w, sy, 1.0),
+             "wgrad": lambda: ops._conv_wgrad(g, x, y, sx, sy, 1.0)}[op]
+        with torch.no_grad():
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 10
+            e0.record()
+            for _ in range(reps):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / reps
+        flop = 2.0 * B * g.OH * g.OW * cin * cout * k * k
+        tot_t += n * t
+        tot_f += n * flop
+        print(f"  {op:5s} B{B:4d} {cin:5d}->{cout:5d} {H:3d}^2 k{k} s{s} {'S' if scaled else ' '}  {t * 1e6:9.1f} us "
+              f"{flop / t / 1e12:7.1f} TF/s", flush=True)
+    print(f"  weighted: {tot_t * 1e3:.1f} ms  {tot_f / tot_t / 1e12:.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--child":
+        child()
+        sys.exit(0)
+    rc = 0
+    for so in sys.argv[1:]:
+        print(f"[{os.path.basename(so)}]", flush=True)
+        env = dict(os.environ, GANAMD_SO=os.path.abspath(so))
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, timeout=300)
+        rc = rc or r.returncode
+        if r.returncode != 0:
+            break
+    sys.exit(rc)
