@@ -59,7 +59,9 @@ constexpr int LDK = BK + 2;   // LDS row stride in floats: 8-byte aligned, b64 r
 constexpr int BKW = GANAMD_BKW; // wgrad K-step (pixels): at 32 a half-wave reads one full 128-byte line
 constexpr int LDKW = BKW + 2;
 
-enum GatherMode { kZero = 0, kReplicate = 1, kTransposed = 2 };
+// kPhase: one output phase (oh % s, ow % s) of a stride-s transposed conv as a stride-1 conv over the
+// input with the (K/s)^2 taps that reach it (Gather.pch/pcw: input offsets of that phase).
+enum GatherMode { kZero = 0, kReplicate = 1, kTransposed = 2, kPhase = 3 };
 
 // Buffer loads: a 32-bit byte offset against a range-checked descriptor.  An offset past the
 // end returns 0 in hardware, so padding / tails are a select of the OFFSET, never a branch
@@ -91,6 +93,7 @@ struct Gather {
   int OH, OW;          // GEMM spatial extents (n = (b, oh, ow))
   int KW, stride, pad;
   int mode;
+  int pch, pcw;        // kPhase: ih = oh + pch - kh, iw = ow + pcw - kw
 
   __device__ int src_bytes() const { return 4 * C * B * H * W; }
   __device__ int scale_bytes() const { return 4 * C * B; }
@@ -99,6 +102,11 @@ struct Gather {
 // Offset of the source pixel feeding output (oh, ow) through tap (kh, kw), or -1 for padding.
 template <int MODE>
 __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int kh, int kw) {
+  if (MODE == kPhase) {
+    const int ih = oh + g.pch - kh, iw = ow + g.pcw - kw;
+    if (ih < 0 || iw < 0 || ih >= g.H || iw >= g.W) return -1;
+    return ih * g.W + iw;
+  }
   if (MODE == kTransposed) {
     int th = oh + g.pad - kh, tw = ow + g.pad - kw;
     if (th < 0 || tw < 0) return -1;
@@ -121,6 +129,17 @@ __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int k
   return ih * g.W + iw;
 }
 
+// Output column of GEMM column n: the identity, or for one phase (qh, qw) of a stride-s transposed
+// conv n = (b, j, i) over the OHp x OWp phase grid -> (b, s*j + qh, s*i + qw) of the OH x OW output.
+struct OutMap {
+  int s, qh, qw, OWp, ohwp, OW, OHW;
+};
+__device__ __forceinline__ long out_col(const OutMap& r, int n) {
+  if (r.s == 0) return n;
+  const int b = n / r.ohwp, q = n - b * r.ohwp, j = q / r.OWp, i = q - j * r.OWp;
+  return (long)b * r.OHW + (long)(r.s * j + r.qh) * r.OW + r.s * i + r.qw;
+}
+
 struct ConvArgs {
   const float* w;      // packed A[Mpad][T][Ckp] (see pack_a_kernel); before packing A(m,t,c) = w[m*sm + c*sc + t*st]
   int sm, sc, st, w_bytes;
@@ -141,6 +160,8 @@ struct ConvArgs {
   int tail_n0, tail_cols;  // first tail column (pixel) and the tail width
   float* slab;         // S > 1: per-split partial tail tiles [S][M][tail_cols]
   int bf16;            // GANAMD_MATH_BF16: operands rounded to bf16, fp32 accumulation
+  OutMap om;           // GEMM column -> output column (identity unless kPhase)
+  long ldy;            // row length of y (N unless kPhase: the full B*OH*OW)
 };
 
 struct WgradArgs {
@@ -259,20 +280,37 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
 // its pixels + halo, ~13 KB) stay in L1/L2; tap-outer order would cycle every channel through
 // the cache between re-reads (the working set of the resident blocks of an XCD then exceeds
 // its 4 MB L2 on the 64-128-channel maps).
-__global__ void pack_a_kernel(const float* __restrict__ w, int sm, int sc, int st, int M, int Ck, int T, int Mpad,
-                              int Ckp, float* __restrict__ out) {
-  const long total = (long)Mpad * T * Ckp;
-  const int nct = Ckp / BK;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c16 = (int)(i % BK);
-    const long r = i / BK;
-    const int t = (int)(r % T);
-    const long r2 = r / T;
-    const int cc = (int)(r2 % nct);
-    const int m = (int)(r2 / nct);
-    const int c = cc * BK + c16;
-    out[i] = (m < M && c < Ck) ? w[(long)m * sm + (long)c * sc + (long)t * st] : 0.f;
+// Element i of a job's GEMM-order output.  ps > 1: the s*s phases of a stride-s transposed conv
+// one after another, phase q = (qh, qw) over its (K/s)^2 taps t' = (a, b) -> kernel tap
+// (kh0 + s*a, kw0 + s*b) with kh0 = (qh + pad) % s (see kPhase).
+__device__ __forceinline__ float pack_elem(const ganamd_pack_job& j, long i) {
+  const int nct = j.Ckp / BK;
+  int T = j.T, q = 0;
+  if (j.ps > 1) {
+    T = j.T / (j.ps * j.ps);
+    const long per = (long)j.Mpad * T * j.Ckp;
+    q = (int)(i / per);
+    i -= q * per;
   }
+  const int c16 = (int)(i % BK);
+  const long r = i / BK;
+  int t = (int)(r % T);
+  const long r2 = r / T;
+  const int cc = (int)(r2 % nct);
+  const int m = (int)(r2 / nct);
+  const int c = cc * BK + c16;
+  if (j.ps > 1) {
+    const int kk = j.pk / j.ps, qh = q / j.ps, qw = q - qh * j.ps;
+    const int kh = (qh + j.ppad) % j.ps + j.ps * (t / kk), kw = (qw + j.ppad) % j.ps + j.ps * (t % kk);
+    t = kh * j.pk + kw;
+  }
+  return (m < j.M && c < j.Ck) ? j.w[(long)m * j.sm + (long)c * j.sc + (long)t * j.st] : 0.f;
+}
+
+__global__ void pack_a_kernel(ganamd_pack_job j) {
+  const long total = (long)j.Mpad * j.T * j.Ckp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+    j.out[i] = pack_elem(j, i);
 }
 
 #ifndef GANAMD_CONV_WPE
@@ -344,8 +382,11 @@ void conv_gemm_kernel(ConvArgs p) {
   const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
   const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
 
-  f32x4 ra[EA];
-  float rb[KPT], rs[KPT];
+  // one K-step's operands in flight: the A slots and the B gather (+ its per-(channel, sample) scales)
+  struct Stage {
+    f32x4 ra[EA];
+    float rb[KPT], rs[KPT];
+  };
   // (cc, kh, kw): channel chunk and tap of the next K-step to load (k = (cc, t, c16))
   int cc = kt0 / p.T;
   int kh, kw;
@@ -357,18 +398,18 @@ void conv_gemm_kernel(ConvArgs p) {
   auto tap = [&]() { return n_ok ? tap_offset<MODE>(g, oh, ow, kh, kw) : -1; };
   int sp = tap();
 
-  auto gload = [&](int kt) {
+  auto gload = [&](int kt, Stage& S) {
 #pragma unroll
     for (int e = 0; e < EA; ++e)
-      if (tid + e * kThreads < A4) ra[e] = bload4(rw, a_off[e] + kt * (BK * 4));
+      if (tid + e * kThreads < A4) S.ra[e] = bload4(rw, a_off[e] + kt * (BK * 4));
     const int c = cc * BK + b_kg * KPT;
     // channels past the source's end fall outside the buffer: the hardware returns 0
     const unsigned base = sp >= 0 ? 4u * (unsigned)(img + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
     const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + bb) : (unsigned)kOOB;
 #pragma unroll
     for (int e = 0; e < KPT; ++e) {
-      rb[e] = bload(rx, (int)(base + (unsigned)e * cs4));
-      if (BSCALE) rs[e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
+      S.rb[e] = bload(rx, (int)(base + (unsigned)e * cs4));
+      if (BSCALE) S.rs[e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
     }
     if (++kw == g.KW) {
       kw = 0;
@@ -379,7 +420,10 @@ void conv_gemm_kernel(ConvArgs p) {
     }
     sp = tap();
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const Stage& S) {
+    const f32x4* ra = S.ra;
+    const float* rb = S.rb;
+    const float* rs = S.rs;
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       const int slot = tid + e * kThreads;
@@ -413,29 +457,58 @@ void conv_gemm_kernel(ConvArgs p) {
   f32x16 acc[C::TM][C::TN];
   zero_acc<C>(acc);
 
-  gload(kt0);
-  sstore(0);
+  Stage s0;
+#ifndef GANAMD_NO_PF2
+  // two K-steps in flight: the gather for step kt+2 is issued while step kt's MFMAs run and step
+  // kt+1's operands (loaded one step earlier) go to LDS -- twice the latency cover per wave
+  Stage s1;
+  gload(kt0, s0);
+  sstore(0, s0);
+  if (kt0 + 1 < kt1) gload(kt0 + 1, s1);
+  __syncthreads();
+  int kt = kt0;
+  for (; kt + 1 < kt1; kt += 2) {
+    if (kt + 2 < kt1) gload(kt + 2, s0);
+#pragma unroll
+    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[0], Bs[0], acc, lane, wm, wn, k0);
+    sstore(1, s1);
+    __syncthreads();
+    if (kt + 3 < kt1) gload(kt + 3, s1);
+#pragma unroll
+    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[1], Bs[1], acc, lane, wm, wn, k0);
+    if (kt + 2 < kt1) sstore(0, s0);
+    __syncthreads();
+  }
+  if (kt < kt1) {
+#pragma unroll
+    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[0], Bs[0], acc, lane, wm, wn, k0);
+  }
+#else
+  gload(kt0, s0);
+  sstore(0, s0);
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
-    if (more) gload(kt + 1);
+    if (more) gload(kt + 1, s0);
 #pragma unroll
     for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
-    if (more) sstore(buf ^ 1);
+    if (more) sstore(buf ^ 1, s0);
     __syncthreads();
   }
+#endif
 
   // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // Split-K blocks store raw partial tiles to their slab; the reduce kernel applies the rest.
   const bool finish = split < 0 || p.S == 1;
   float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
-  const long ldo = finish ? p.N : p.tail_cols;
+  const long ldo = finish ? p.ldy : p.tail_cols;
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
     const int n = n0 + (wn * C::TN + j) * 32 + (lane & 31);
     if (n >= p.N) continue;
     const int b = (finish && p.oscale) ? n / p.ohw : 0;
+    const long col = (MODE == kPhase && finish) ? out_col(p.om, n) : n;
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
@@ -446,10 +519,10 @@ void conv_gemm_kernel(ConvArgs p) {
         if (finish) {
           if (p.oscale) v *= p.oscale[m * g.B + b];
           if (p.bias) v += p.bias[m];
-          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.N + n];
+          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
           if (p.act) v = v > 0.f ? v : p.act[m] * v;
         }
-        out[(long)m * ldo + n] = v;
+        out[(long)m * ldo + col] = v;
       }
     }
   }
@@ -469,17 +542,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
   const ganamd_pack_job j = jobs[lo];
   const long total = (long)j.Mpad * j.T * j.Ckp;
   const long i0 = (b - j.chunk0) * kPackChunk;
-  const int nct = j.Ckp / BK;
-  for (long i = i0 + threadIdx.x; i < min(total, i0 + kPackChunk); i += 256) {
-    const int c16 = (int)(i % BK);
-    const long r = i / BK;
-    const int t = (int)(r % j.T);
-    const long r2 = r / j.T;
-    const int cc = (int)(r2 % nct);
-    const int m = (int)(r2 / nct);
-    const int c = cc * BK + c16;
-    j.out[i] = (m < j.M && c < j.Ck) ? j.w[(long)m * j.sm + (long)c * j.sc + (long)t * j.st] : 0.f;
-  }
+  for (long i = i0 + threadIdx.x; i < min(total, i0 + kPackChunk); i += 256) j.out[i] = pack_elem(j, i);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -722,6 +785,16 @@ int splitk_enabled() {   // GANAMD_SPLITK=0 disables split-K (experiments)
   static const int v = env_int("GANAMD_SPLITK", 1);
   return v;
 }
+// Unused dynamic LDS per conv / wgrad block (bytes): caps the resident blocks per CU, i.e. the
+// waves per SIMD (occupancy experiments: GANAMD_CONV_LDS_PAD, GANAMD_WGRAD_LDS_PAD).
+int conv_lds_pad() {
+  static const int v = env_int("GANAMD_CONV_LDS_PAD", 0);
+  return v;
+}
+int wgrad_lds_pad() {
+  static const int v = env_int("GANAMD_WGRAD_LDS_PAD", 0);
+  return v;
+}
 
 
 // Split-K planning.  Splits exist only to fill the chip when the output tile grid is small;
@@ -733,7 +806,11 @@ struct Plan {
 };
 
 int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
-int conv_bn(int bm, int) { return bm == 32 ? 256 : 128; }
+int wide_tiles() {   // GANAMD_WIDE=1: 128 x 256 tiles (2 waves per SIMD) for M > 96 (A/B experiments)
+  static const int v = env_int("GANAMD_WIDE", 0);
+  return v;
+}
+int conv_bn(int bm, int) { return bm == 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
 
 // Split-K: pure functions of the geometry (the workspace query and the launch agree).
@@ -806,7 +883,7 @@ int conv_occ() {
   static const int v = [] {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, BF16>, kThreads,
-                                                     0) != hipSuccess || n <= 0)
+                                                     conv_lds_pad()) != hipSuccess || n <= 0)
       n = 2;
     return n;
   }();
@@ -819,7 +896,7 @@ int conv_occ_tile(int bm, int bn) {
     case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE, BF16>();
     case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
     case 96: return conv_occ<96, 128, 1, 4, MODE, BSCALE, BF16>();
-    default: return conv_occ<128, 128, 2, 2, MODE, BSCALE, BF16>();
+    default: return bn == 256 ? conv_occ<128, 256, 2, 2, MODE, BSCALE, BF16>() : conv_occ<128, 128, 2, 2, MODE, BSCALE, BF16>();
   }
 }
 
@@ -938,7 +1015,7 @@ int wgrad_occ() {
   static const int v = [] {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wgrad_gemm_kernel<BM, BN, WGM, WGN, kReplicate, SCALED, false>,
-                                                     kThreads, 0) != hipSuccess || n <= 0)
+                                                     kThreads, wgrad_lds_pad()) != hipSuccess || n <= 0)
       n = 2;
     return n;
   }();
@@ -968,18 +1045,19 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
 }
 
 // Folds the S partial slabs of the tail columns [n0, n0 + cols) and applies the epilogue.
-__global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int cols, int n0, int N,
+__global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int cols, int n0, long ldy,
                                          int ohw, int B, const float* __restrict__ oscale,
                                          const float* __restrict__ bias, const float* __restrict__ noise,
                                          const float* __restrict__ noise_scale, const float* __restrict__ act,
-                                         float* __restrict__ y) {
+                                         float* __restrict__ y, OutMap om) {
   const long total = (long)M * cols;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += slab[s * total + i];
     const int m = (int)(i / cols);
-    const long o = (long)m * N + n0 + (i - (long)m * cols);
-    if (oscale) v *= oscale[m * B + (int)(o % N) / ohw];
+    const int n = n0 + (int)(i - (long)m * cols);
+    const long o = (long)m * ldy + out_col(om, n);
+    if (oscale) v *= oscale[m * B + n / ohw];
     if (bias) v += bias[m];
     if (noise) v += noise_scale[m] * noise[o];
     if (act) v = v > 0.f ? v : act[m] * v;
@@ -1009,12 +1087,12 @@ hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t 
   p.tail_cols = std::max(0, p.N - p.tail_n0);
   p.slab = pl.slab_elems ? slab : nullptr;
   const long blocks = (long)p.full_blocks + (long)(pl.gx - pl.nfull_t) * pl.gy * pl.S;
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, BF16>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                     st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, BF16>), dim3((unsigned)blocks), dim3(kThreads),
+                     conv_lds_pad(), st, p);
   if (pl.slab_elems)
     hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.tail_cols)), dim3(256), 0, st, slab, pl.S,
-                       p.M, p.tail_cols, p.tail_n0, p.N, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
-                       p.y);
+                       p.M, p.tail_cols, p.tail_n0, p.ldy, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
+                       p.y, p.om);
   return hipGetLastError();
 }
 
@@ -1024,13 +1102,14 @@ hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab
     case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
     case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
-    default: return launch_conv<128, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
+    default:
+      return pl.bn == 256 ? launch_conv<128, 256, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st)
+                          : launch_conv<128, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
   }
 }
 
-void launch_pack(const ConvArgs& p, int mpad, int ckp, float* packed, hipStream_t st) {
-  hipLaunchKernelGGL(pack_a_kernel, dim3(grid1d((long)mpad * p.T * ckp)), dim3(256), 0, st, p.w, p.sm, p.sc, p.st,
-                     p.M, p.Ck, p.T, mpad, ckp, packed);
+void launch_pack(const ganamd_pack_job& j, hipStream_t st) {
+  hipLaunchKernelGGL(pack_a_kernel, dim3(grid1d((long)j.Mpad * j.T * j.Ckp)), dim3(256), 0, st, j);
 }
 
 template <bool BF16>
@@ -1042,6 +1121,8 @@ hipError_t dispatch_conv_mode(const ConvArgs& p, const ConvPlan& pl, float* slab
     case kReplicate:
       return s ? dispatch_conv_tile<kReplicate, true, BF16>(p, pl, slab, st)
                : dispatch_conv_tile<kReplicate, false, BF16>(p, pl, slab, st);
+    case kPhase:   // unmodulated only (ConvTranspose2d)
+      return s ? hipErrorInvalidValue : dispatch_conv_tile<kPhase, false, BF16>(p, pl, slab, st);
     default:
       return s ? dispatch_conv_tile<kTransposed, true, BF16>(p, pl, slab, st)
                : dispatch_conv_tile<kTransposed, false, BF16>(p, pl, slab, st);
@@ -1055,8 +1136,9 @@ hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab,
   if ((pl.slab_elems && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
   const int mpad = (p.M + pl.bm - 1) / pl.bm * pl.bm;
   p.Ckp = (p.Ck + BK - 1) / BK * BK;
+  if (p.ldy == 0) p.ldy = p.N;   // output rows are the GEMM rows unless a phase remap says otherwise
   if (!prepacked) {
-    launch_pack(p, mpad, p.Ckp, packed, st);
+    launch_pack(ganamd_pack_job{p.w, packed, p.sm, p.sc, p.st, p.M, p.Ck, p.T, mpad, p.Ckp, 1, 0, 0, 0}, st);
     p.w = packed;
   }
   p.w_bytes = 4 * mpad * p.T * p.Ckp;
@@ -1071,7 +1153,7 @@ hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStre
   p.splits = pl.splits;
   p.slab = pl.splits > 1 ? slab : nullptr;
   hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED, BF16>), dim3(gx, gy, T * pl.splits), dim3(kThreads),
-                     0, st, p);
+                     wgrad_lds_pad(), st, p);
   if (pl.splits > 1)
     hipLaunchKernelGGL(wgrad_split_reduce_kernel, dim3(grid1d(p.out_numel)), dim3(256), 0, st, slab, pl.splits,
                        p.out_numel, p.out, p.accumulate);
@@ -1136,11 +1218,14 @@ bool desc_ok(const ganamd_conv_desc* d) {
 extern "C" {
 
 // Geometry of each GEMM the three entry points issue (shared by the workspace query and launch).
+static bool fwd_phased(const ganamd_conv_desc* d);
+// (phased: the GEMM of ONE output phase; there are stride^2 of them)
 static void fwd_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T) {
+  const int s2 = fwd_phased(d) ? d->stride * d->stride : 1;
   *M = d->Cout;
-  *N = d->B * d->OH * d->OW;
+  *N = d->B * d->OH * d->OW / s2;
   *Ck = d->Cin;
-  *T = d->KH * d->KW;
+  *T = d->KH * d->KW / s2;
 }
 
 // Small maps (<= 10x10) and strided convs: dgrad as a plain GEMM over the conv's OUTPUT pixels,
@@ -1202,6 +1287,23 @@ static void a_operand(const ganamd_conv_desc* d, int op, int* M, int* Ck, int* T
   }
 }
 
+// Forward of a stride-s transposed conv as s*s phase GEMMs (kPhase): each output phase
+// (oh % s, ow % s) sees only (K/s)^2 of the K^2 taps, so the transposed gather's zero taps
+// (3 in 4 at s = 2) never reach the MFMAs.
+static bool fwd_phased(const ganamd_conv_desc* d) {
+  return d->transposed && d->stride > 1 && d->KH == d->KW && d->KH % d->stride == 0 && d->OH % d->stride == 0 &&
+         d->OW % d->stride == 0;
+}
+
+static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed) {
+  int M, Ck, T, sm, sc, bm, bn;
+  a_operand(d, op, &M, &Ck, &T, &sm, &sc);
+  conv_tile(M, &bm, &bn);
+  const bool ph = op == GANAMD_CONV_FWD && fwd_phased(d);
+  return ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, (M + bm - 1) / bm * bm, (Ck + BK - 1) / BK * BK,
+                         ph ? d->stride : 1, ph ? d->KH : 0, ph ? d->pad : 0, 0};
+}
+
 static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
   if (d->transposed || d->pad == 0 || dgrad_scatter(d)) return 0;
   return sizeof(float) * (size_t)d->Cin * d->B * (d->H + 2 * d->pad) * (d->W + 2 * d->pad);
@@ -1212,6 +1314,7 @@ static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Gather mode of the fwd / dgrad GEMM; the split slabs the plan needs, for either scale variant
 // (the query does not know whether a scale will be passed; the launch plans with the actual one).
 static int fwd_mode(const ganamd_conv_desc* d) {
+  if (fwd_phased(d)) return kPhase;
   return d->transposed ? kTransposed : (d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero);
 }
 static int dgrad_mode(const ganamd_conv_desc* d) { return (dgrad_scatter(d) || d->transposed) ? kZero : kTransposed; }
@@ -1247,10 +1350,7 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
 
 int ganamd_conv_pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed, ganamd_pack_job* job) {
   if (!desc_ok(d) || !w || !packed || !job || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
-  int M, Ck, T, sm, sc, bm, bn;
-  a_operand(d, op, &M, &Ck, &T, &sm, &sc);
-  conv_tile(M, &bm, &bn);
-  *job = ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, (M + bm - 1) / bm * bm, (Ck + BK - 1) / BK * BK, 0};
+  *job = pack_job(d, op, w, packed);
   return GANAMD_OK;
 }
 
@@ -1268,16 +1368,7 @@ int ganamd_conv_pack_batch(const ganamd_pack_job* jobs, int n_jobs, int64_t tota
 
 int ganamd_conv_pack(const ganamd_conv_desc* d, int op, const float* w, float* packed, hipStream_t stream) {
   if (!desc_ok(d) || !w || !packed || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
-  ConvArgs p{};
-  int sm, sc;
-  a_operand(d, op, &p.M, &p.Ck, &p.T, &sm, &sc);
-  p.w = w;
-  p.sm = sm;
-  p.sc = sc;
-  p.st = 1;
-  int bm, bn;
-  conv_tile(p.M, &bm, &bn);
-  launch_pack(p, (p.M + bm - 1) / bm * bm, (p.Ck + BK - 1) / BK * BK, packed, stream);
+  launch_pack(pack_job(d, op, w, packed), stream);
   return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
@@ -1287,7 +1378,8 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   *bytes = 0;
   if (op == GANAMD_CONV_FWD) {
     fwd_gemm(d, &M, &N, &Ck, &T);
-    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + slab_bytes(M, N, Ck, T, fwd_mode(d), d->math == GANAMD_MATH_BF16);
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, d->KH * d->KW))) +
+             slab_bytes(M, N, Ck, T, fwd_mode(d), d->math == GANAMD_MATH_BF16);
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
@@ -1323,6 +1415,7 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   ConvArgs p{};
   int M, N, Ck, T, sm, sc;
   fwd_gemm(d, &M, &N, &Ck, &T);
+  const int Nph = N, Tph = T;
   a_operand(d, GANAMD_CONV_FWD, &M, &Ck, &T, &sm, &sc);
   p.w = w;
   p.sm = sm;
@@ -1343,10 +1436,37 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   p.N = N;
   p.ohw = d->OH * d->OW;
   p.bf16 = d->math == GANAMD_MATH_BF16;
+  p.ldy = N;
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
   float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))));
-  return dispatch_conv(p, d->packed_w != 0, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  if (!fwd_phased(d))
+    return dispatch_conv(p, d->packed_w != 0, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  if (x_scale || y_scale) return GANAMD_EINVAL;   // phased transposed convs are unmodulated
+  // s*s phase GEMMs over the phase-packed weights (pack_job): phase q = (qh, qw) writes the
+  // outputs (b, s*j + qh, s*i + qw) of its OHp x OWp grid
+  const int s = d->stride, OHp = d->OH / s, OWp = d->OW / s;
+  const float* wq = w;
+  if (!d->packed_w) {
+    launch_pack(pack_job(d, GANAMD_CONV_FWD, w, packed), stream);
+    wq = packed;
+  }
+  int bm, bn;
+  conv_tile(M, &bm, &bn);
+  const long per = (long)((M + bm - 1) / bm * bm) * Tph * ((Ck + BK - 1) / BK * BK);
+  p.T = Tph;
+  p.N = Nph;
+  p.ohw = OHp * OWp;
+  p.ldy = (long)d->B * d->OH * d->OW;
+  for (int q = 0; q < s * s; ++q) {
+    const int qh = q / s, qw = q % s, kh0 = (qh + d->pad) % s, kw0 = (qw + d->pad) % s;
+    p.w = wq + q * per;
+    p.g = Gather{x, nullptr, d->Cin, d->B, d->H, d->W, OHp, OWp, d->KW / s, 1, 0, kPhase,
+                 (qh + d->pad - kh0) / s, (qw + d->pad - kw0) / s};
+    p.om = OutMap{s, qh, qw, OWp, OHp * OWp, d->OW, d->OH * d->OW};
+    if (dispatch_conv(p, true, nullptr, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+  }
+  return GANAMD_OK;
 }
 
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale, float alpha,

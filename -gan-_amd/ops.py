@@ -114,21 +114,51 @@ def linear_geo(B, cin, cout):
 
 
 class FlopCounter:
-    """Counts MFMA-GEMM FLOPs issued through the conv wrappers while ``enabled`` (host side;
-    used by bench.py on an eager iteration to report executed vs algorithmic work)."""
+    """Counts the conv-GEMM FLOPs issued through the conv wrappers while ``enabled`` (host side;
+    used by bench.py on an eager iteration to report executed vs algorithmic work).
+
+    ``flops`` is what the MFMAs execute: a stride-s transposed conv's forward runs as s^2 phase
+    GEMMs over only the taps that reach each output phase (the algorithmic work; a geometry the
+    phase split does not cover runs the transposed gather, every tap at every OUTPUT pixel), the
+    stride-1 transposed-gather dgrad runs over the padded frame; ``algo_flops`` is the algorithmic
+    count 2 * MACs.  ``flops_bf16`` is the part issued in bf16 math."""
 
     enabled = False
     flops = 0
+    algo_flops = 0
+    flops_bf16 = 0
     launches = 0
     record = None          # optional list receiving (op, geo, has_xscale, has_yscale)
+
+    @staticmethod
+    def algorithmic(geo: "Geo") -> int:
+        sp = geo.H * geo.W if geo.transposed else geo.OH * geo.OW
+        return 2 * geo.B * sp * geo.Cout * geo.Cin * geo.K * geo.K
+
+    @staticmethod
+    def issued(geo: "Geo", op: str) -> int:
+        macs_per_px = geo.Cout * geo.Cin * geo.K * geo.K
+        if op == "fwd" and geo.transposed:
+            s = geo.stride
+            if s > 1 and geo.K % s == 0 and geo.OH % s == 0 and geo.OW % s == 0:
+                # phase-decomposed (csrc/conv_gemm.hip kPhase): s^2 GEMMs of (K/s)^2 taps each
+                return 2 * geo.B * geo.OH * geo.OW * macs_per_px // (s * s)
+            return 2 * geo.B * geo.OH * geo.OW * macs_per_px
+        if op == "dgrad" and not geo.transposed and geo.K > 1 and not (geo.stride > 1 or geo.H * geo.W <= 100):
+            # transposed gather into the padded frame (csrc/conv_gemm.hip dgrad_gemm)
+            return 2 * geo.B * (geo.H + 2 * geo.pad) * (geo.W + 2 * geo.pad) * macs_per_px
+        return FlopCounter.algorithmic(geo)
 
     @classmethod
     def add(cls, geo: "Geo", op: str = "", xs=False, ys=False):
         if cls.record is not None:
             cls.record.append((op, geo, xs, ys))
         if cls.enabled:
-            cls.flops += 2 * geo.B * geo.OH * geo.OW * geo.Cout * geo.Cin * geo.K * geo.K if not geo.transposed \
-                else 2 * geo.B * geo.H * geo.W * geo.Cout * geo.Cin * geo.K * geo.K
+            f = cls.issued(geo, op)
+            cls.flops += f
+            cls.algo_flops += cls.algorithmic(geo)
+            if _MATH[0] == _lib.MATH_BF16:
+                cls.flops_bf16 += f
             cls.launches += 1
 
 

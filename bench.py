@@ -37,6 +37,7 @@ sys.path.insert(0, REPO)
 METRIC = "images/sec per WGAN-GP iter (G13_5+D9_4, 64x64, n_critic=5) at 1/2/4/8 MI355X"
 ALGO_GFLOP_PER_IMAGE = 1559.5
 FP32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md, chip-level parameters
+BF16_MFMA_PEAK_TFLOPS = 2500.0         # dense bf16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
 N_CRITIC = 5
 
 
@@ -189,6 +190,65 @@ def roofline_probe(dev, reps=20):
     return out
 
 
+def bf16_algo(algo, issued, bf16_issued):
+    """Algorithmic FLOPs of the bf16 part (issued bf16 scaled by the algorithmic/issued ratio)."""
+    return bf16_issued * (algo / issued) if issued else 0.0
+
+
+def gemm_census(dev, rec, top=8):
+    """Per-shape speed of the iteration's conv GEMMs: every distinct (op, geometry, scales) recorded
+    in one eager iteration is timed in isolation (HIP events around 5 back-to-back launches after a
+    warm-up) on the bench's own stream; est time = count x time.  Returns the GEMM-weighted
+    achieved TF/s (algorithmic FLOPs / est time), its fraction of the fp32 MFMA peak, and the top
+    shapes by estimated time with their own fractions."""
+    import collections
+    import gan_amd.ops as ops
+    cnt = collections.Counter(rec)
+    rows = []
+    s = torch.cuda.current_stream()
+    for (op, g, xs, ys), n in cnt.items():
+        xin = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
+        yout = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
+        w = torch.nn.Parameter(torch.randn((g.Cin, g.Cout, g.K, g.K) if g.transposed else (g.Cout, g.Cin, g.K, g.K),
+                                           device=dev))
+        sx = torch.rand(g.Cin, g.B, device=dev) if xs else None
+        sy = torch.rand(g.Cout, g.B, device=dev) if ys else None
+        if op == "fwd":
+            f = lambda: ops._conv_fwd(g, xin, w, None, sx, sy, 1.0)
+        elif op == "dgrad":      # the recorded flag is the gy (Cout-side) scale
+            sgy = torch.rand(g.Cout, g.B, device=dev) if xs else None
+            f = lambda: ops._conv_dgrad(g, yout, w, sgy, 1.0)
+        else:
+            f = lambda: ops._conv_wgrad(g, xin, yout, sx, sy, 1.0)
+        with torch.no_grad():
+            f()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(5):
+                f()
+            e1.record(s)
+            torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 5e3
+        flop = ops.FlopCounter.algorithmic(g)
+        rows.append((n * t, n, t, flop, op, g, xs or ys))
+        del xin, yout, w, sx, sy
+    rows.sort(key=lambda r: -r[0])
+    tot_t = sum(r[0] for r in rows)
+    tot_f = sum(r[1] * r[3] for r in rows)
+    tf = tot_f / tot_t / 1e12
+
+    def shape(r):
+        g = r[5]
+        return (f"{r[4]} B={g.B} {g.Cin}->{g.Cout} {g.H}x{g.W}->{g.OH}x{g.OW} k{g.K} s{g.stride}"
+                f"{' T' if g.transposed else ''}{' scaled' if r[6] else ''}")
+    return {"distinct_shapes": len(rows), "launches_per_iter": sum(r[1] for r in rows),
+            "est_gemm_s_per_iter": tot_t, "gemm_tflops": tf, "gemm_frac": tf / FP32_MFMA_PEAK_TFLOPS,
+            "method": "every distinct conv GEMM of one iteration timed in isolation (HIP events, 5 launches); "
+                      "algorithmic FLOPs / (count x time); includes each op's split-K reduce / fold launches",
+            "top": [{"shape": shape(r), "count": r[1], "us": 1e6 * r[2], "tflops": r[3] / r[2] / 1e12,
+                     "frac": r[3] / r[2] / 1e12 / FP32_MFMA_PEAK_TFLOPS, "share": r[0] / tot_t} for r in rows[:top]]}
+
+
 CONFIGS = {
     # name: (metric, default per-GPU batch, description)
     "wgangp": (METRIC, 64, "G13_5+D9_4 WGAN-GP iteration (5 critic steps with GP + 1 generator step), 64x64x3"),
@@ -270,9 +330,12 @@ def main():
 
     # warm-up (eager); the first one also counts the conv FLOPs this build issues
     ops.FlopCounter.enabled = True
+    census_rec = ops.FlopCounter.record = []
     iteration()
     ops.FlopCounter.enabled = False
+    ops.FlopCounter.record = None
     issued_flops = ops.FlopCounter.flops
+    algo_flops, bf16_flops = ops.FlopCounter.algo_flops, ops.FlopCounter.flops_bf16
     for _ in range(max(0, args.warmup - 1)):
         iteration()
     torch.cuda.synchronize()
@@ -393,9 +456,11 @@ def main():
             torch.cuda.synchronize()
             parts[key] = round(e0.elapsed_time(e1), 1)
         print(f"[bench] ms per phase graph: {parts}", file=sys.stderr, flush=True)
-    probe = None
+    probe = census = None
     if rank == 0 and world == 1 and headline and not args.no_extras:
         probe = roofline_probe(dev)
+    if rank == 0 and world == 1 and not args.no_extras:
+        census = gemm_census(dev, census_rec)
     if rank == 0:
         print(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB "
               f"(reserved {torch.cuda.max_memory_reserved() / 2**30:.1f}), "
@@ -426,12 +491,23 @@ def main():
                 # whole iteration: algorithmic FLOPs / iteration time, per GPU
                 "iteration_tflops": achieved, "iteration_frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                 "algorithmic_gflop_per_iter": ALGO_GFLOP_PER_IMAGE * B,
+                "algorithmic_gemm_gflop_per_iter": algo_flops / 1e9,
                 "issued_gemm_gflop_per_iter": issued_flops / 1e9})
         else:
-            out["roofline"] = {"bound": "mfma", "issued_gemm_gflop_per_iter": issued_flops / 1e9,
-                               "achieved": issued_flops / t_iter / 1e12, "peak": FP32_MFMA_PEAK_TFLOPS,
-                               "unit": "TFLOP/s", "frac": issued_flops / t_iter / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                               "note": "issued conv-GEMM FLOPs of this build per iteration / iteration time"}
+            # bf16 and fp32 GEMMs priced at their own peaks: frac = (time the issued-precision mix
+            # needs at peak) / iteration time; "peak" is that mix's effective rate
+            t_peak = (algo_flops - bf16_algo(algo_flops, issued_flops, bf16_flops)) / (FP32_MFMA_PEAK_TFLOPS * 1e12) + \
+                bf16_algo(algo_flops, issued_flops, bf16_flops) / (BF16_MFMA_PEAK_TFLOPS * 1e12)
+            eff_peak = algo_flops / t_peak / 1e12
+            out["roofline"] = {"bound": "mfma", "algorithmic_gemm_gflop_per_iter": algo_flops / 1e9,
+                               "issued_gemm_gflop_per_iter": issued_flops / 1e9,
+                               "bf16_issued_gemm_gflop_per_iter": bf16_flops / 1e9,
+                               "achieved": algo_flops / t_iter / 1e12, "peak": eff_peak, "unit": "TFLOP/s",
+                               "frac": algo_flops / t_iter / 1e12 / eff_peak,
+                               "note": "algorithmic conv-GEMM FLOPs per iteration / iteration time, against the "
+                                       "fp32 (157.3) / bf16 (2500) MFMA peaks weighted by the FLOPs each precision runs"}
+        if census is not None:
+            out["roofline"]["gemm_census"] = census
         out["wall_s"] = wall
         if world == 1 and headline and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)

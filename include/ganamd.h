@@ -84,6 +84,8 @@ typedef struct ganamd_pack_job {
   const float* w;
   float* out;
   int32_t sm, sc, st, M, Ck, T, Mpad, Ckp;
+  int32_t ps, pk, ppad;   /* ps > 1: the s*s output phases of a stride-ps transposed conv (kernel pk,
+                             padding ppad), each packed over its (pk/ps)^2 taps; T counts all pk^2 */
   int64_t chunk0;
 } ganamd_pack_job;
 int ganamd_conv_pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed, ganamd_pack_job* job);

@@ -1,6 +1,7 @@
 """A/B timing of the iteration's dominant GEMM shapes across library builds.
 
-    python tools/ab_shapes.py LIB1.so [LIB2.so ...]      (each build in its own child process)
+    python tools/ab_shapes.py LIB1.so[:VAR=V,VAR2=V] [LIB2.so ...]   (each in its own child process,
+                                                                     with those environment variables)
 
 Shapes: the largest GEMMs of one WGAN-GP iteration at B=64 (profiles/*census*): generator
 modulated convs (scaled), critic block convs on the 2B = 128 real+fake batch, their dgrad / wgrad,
@@ -68,9 +69,11 @@ if __name__ == "__main__":
         child()
         sys.exit(0)
     rc = 0
-    for so in sys.argv[1:]:
-        print(f"[{os.path.basename(so)}]", flush=True)
+    for arg in sys.argv[1:]:
+        so, _, kv = arg.partition(":")
+        print(f"[{os.path.basename(so)} {kv}]", flush=True)
         env = dict(os.environ, GANAMD_SO=os.path.abspath(so))
+        env.update(dict(x.split("=", 1) for x in kv.split(",") if x))
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, timeout=300)
         rc = rc or r.returncode
         if r.returncode != 0:
