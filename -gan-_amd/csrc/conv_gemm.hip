@@ -313,15 +313,237 @@ __global__ void pack_a_kernel(ganamd_pack_job j) {
     j.out[i] = pack_elem(j, i);
 }
 
+
+// ---- bf16 operands in LDS (GANAMD_MATH_BF16, config 4) --------------------------------------
+// The same GEMM with both operand tiles staged in LDS as bf16 (RNE from the fp32 packed weights
+// and the fp32 gather, scales applied first): a K-step of 32 = two of the fp32 path's 16-wide
+// steps (consecutive (channel chunk, tap) pairs of the packed K order), 80-byte LDS rows read
+// with one ds_read_b128 per lane per fragment, one v_mfma_f32_32x32x16_bf16 per 16 k.  Half the
+// LDS bytes of the fp32 tile per k, a quarter of the LDS read instructions; fp32 accumulation and
+// epilogue as in the fp32 kernel.
+constexpr int BKB = 32;        // bf16 K-step
+constexpr int LDB = BKB + 8;   // LDS row stride (bf16 elements): 80 B, 16-B aligned, ds_read_b128 conflict-free
+
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ u16x8 to_bf16x8(const float* v) {
+  bf16x8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = (__bf16)v[e];
+  return __builtin_bit_cast(u16x8, b);
+}
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+__device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
+  using C = TileCfg<BM, BN, WGM, WGN>;
+  constexpr int SA = BM * 4;                          // A slots: 8 consecutive k of one row
+  constexpr int EA = (SA + kThreads - 1) / kThreads;
+  constexpr int H2 = 2 * BN / kThreads;               // 16-k halves per thread (1: BN = 128, 2: BN = 256)
+  static_assert(H2 == 1 || H2 == 2, "B mapping");
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][BM * LDB];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][BN * LDB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int nct = p.Ckp / BK;
+  const int kf_total = nct * p.T;                     // fp32-packed 16-wide K-steps
+  const int kt_total = (kf_total + 1) / 2;            // bf16 K-steps
+  int tx, ty, kt0, kt1, split = -1;
+  {
+    const int bid = blockIdx.x;
+    if (bid < p.full_blocks) {
+      ty = bid % p.gy;
+      tx = bid / p.gy;
+      kt0 = 0;
+      kt1 = kt_total;
+    } else {
+      const int t = bid - p.full_blocks;
+      const int r = t / p.S;
+      split = t - r * p.S;
+      ty = r % p.gy;
+      tx = p.nfull_t + r / p.gy;
+      kt0 = split * p.kt_per_split;
+      kt1 = min(kt_total, kt0 + p.kt_per_split);
+    }
+  }
+  const int n0 = tx * BN, m0 = ty * BM;
+  const int Krow = p.T * p.Ckp;
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  const Gather& g = p.g;
+  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
+  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
+  const int KH = p.T / g.KW;
+
+  // B: pixel n0 + b_n; this thread fills the 16-k halves hb0 .. hb0 + H2 - 1 of every K-step
+  const int b_n = tid % BN, hb0 = (tid / BN) * H2;
+  const int gn = n0 + b_n;
+  const bool n_ok = gn < p.N;
+  int bb = 0, oh = 0, ow = 0;
+  if (n_ok) {
+    bb = gn / p.ohw;
+    const int rr = gn - bb * p.ohw;
+    oh = rr / g.OW;
+    ow = rr - oh * g.OW;
+  }
+  const int img = bb * g.H * g.W;
+  // per half: (channel chunk, tap) of its fp32 step f = 2*kt + half, advanced by 2 steps per K-step
+  int hcc[H2], hkh[H2], hkw[H2];
+#pragma unroll
+  for (int h = 0; h < H2; ++h) {
+    const int f = 2 * kt0 + hb0 + h;
+    hcc[h] = f / p.T;
+    const int t = f - hcc[h] * p.T;
+    hkh[h] = t / g.KW;
+    hkw[h] = t - hkh[h] * g.KW;
+  }
+
+  struct Stage {
+    f32x4 ra[EA][2];
+    float rb[H2][16], rs[H2][16];
+  };
+  auto gload = [&](int kt, Stage& S) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int slot = tid + e * kThreads;
+      const int row = slot >> 2, q = slot & 3;          // k = 8q .. 8q+7 of the step
+      const bool ok = slot < SA && 2 * kt + (q >> 1) < kf_total;
+      const int off = ok ? 4 * ((m0 + row) * Krow + kt * BKB + 8 * q) : kOOB;
+      S.ra[e][0] = bload4(rw, off);
+      S.ra[e][1] = bload4(rw, ok ? off + 16 : kOOB);
+    }
+#pragma unroll
+    for (int h = 0; h < H2; ++h) {
+      const int f = 2 * kt + hb0 + h;
+      const int sp = (n_ok && f < kf_total) ? tap_offset<MODE>(g, oh, ow, hkh[h], hkw[h]) : -1;
+      const int c = hcc[h] * BK;
+      const unsigned base = sp >= 0 ? 4u * (unsigned)(img + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
+      const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + bb) : (unsigned)kOOB;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        S.rb[h][e] = bload(rx, (int)(base + (unsigned)e * cs4));
+        if (BSCALE) S.rs[h][e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
+      }
+      // next K-step: two fp32 steps on
+      hkw[h] += 2;
+      while (hkw[h] >= g.KW) {
+        hkw[h] -= g.KW;
+        if (++hkh[h] >= KH) {
+          hkh[h] = 0;
+          ++hcc[h];
+        }
+      }
+    }
+  };
+  auto sstore = [&](int buf, const Stage& S) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int slot = tid + e * kThreads;
+      if (slot < SA) {
+        const float v[8] = {S.ra[e][0][0], S.ra[e][0][1], S.ra[e][0][2], S.ra[e][0][3],
+                            S.ra[e][1][0], S.ra[e][1][1], S.ra[e][1][2], S.ra[e][1][3]};
+        *reinterpret_cast<u16x8*>(&As[buf][(slot >> 2) * LDB + 8 * (slot & 3)]) = to_bf16x8(v);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < H2; ++h) {
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = BSCALE ? S.rb[h][e] * S.rs[h][e] : S.rb[h][e];
+      unsigned short* d = &Bs[buf][b_n * LDB + 16 * (hb0 + h)];
+      *reinterpret_cast<u16x8*>(d) = to_bf16x8(v);
+      *reinterpret_cast<u16x8*>(d + 8) = to_bf16x8(v + 8);
+    }
+  };
+  f32x16 acc[C::TM][C::TN];
+  zero_acc<C>(acc);
+  const int r = lane & 31, hh = lane >> 5;
+  auto mfma_step = [&](int buf) {
+#pragma unroll
+    for (int k0 = 0; k0 < BKB; k0 += 16) {
+      bf16x8 av[C::TM], bv[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+        av[i] = *reinterpret_cast<const bf16x8*>(&As[buf][((wm * C::TM + i) * 32 + r) * LDB + k0 + 8 * hh]);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        bv[j] = *reinterpret_cast<const bf16x8*>(&Bs[buf][((wn * C::TN + j) * 32 + r) * LDB + k0 + 8 * hh]);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  Stage s0, s1;
+  gload(kt0, s0);
+  sstore(0, s0);
+  if (kt0 + 1 < kt1) gload(kt0 + 1, s1);
+  __syncthreads();
+  int kt = kt0;
+  for (; kt + 1 < kt1; kt += 2) {
+    if (kt + 2 < kt1) gload(kt + 2, s0);
+    mfma_step(0);
+    sstore(1, s1);
+    __syncthreads();
+    if (kt + 3 < kt1) gload(kt + 3, s1);
+    mfma_step(1);
+    if (kt + 2 < kt1) sstore(0, s0);
+    __syncthreads();
+  }
+  if (kt < kt1) mfma_step(0);
+
+  const bool finish = split < 0 || p.S == 1;
+  float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
+  const long ldo = finish ? p.ldy : p.tail_cols;
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j) {
+    const int n = n0 + (wn * C::TN + j) * 32 + (lane & 31);
+    if (n >= p.N) continue;
+    const int b = (finish && p.oscale) ? n / p.ohw : 0;
+    const long col = (MODE == kPhase && finish) ? out_col(p.om, n) : n;
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i) {
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int m = m0 + (wm * C::TM + i) * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+        if (m >= p.M) continue;
+        float v = p.alpha * acc[i][j][rr];
+        if (finish) {
+          if (p.oscale) v *= p.oscale[m * g.B + b];
+          if (p.bias) v += p.bias[m];
+          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
+          if (p.act) v = v > 0.f ? v : p.act[m] * v;
+        }
+        out[(long)m * ldo + col] = v;
+      }
+    }
+  }
+}
+
 #ifndef GANAMD_CONV_WPE
 #define GANAMD_CONV_WPE 1
 #endif
 #ifndef GANAMD_WGRAD_WPE
 #define GANAMD_WGRAD_WPE 1
 #endif
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+__device__ __forceinline__ void conv_body_f32(const ConvArgs& p);
+
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD_CONV_WPE)))
 void conv_gemm_kernel(ConvArgs p) {
+  if constexpr (BF16) {
+    conv_body_bf16<BM, BN, WGM, WGN, MODE, BSCALE>(p);
+  } else {
+    conv_body_f32<BM, BN, WGM, WGN, MODE, BSCALE>(p);
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+__device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
+  constexpr bool BF16 = false;
   using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int A4 = BM * BK / 4;                      // 16-byte slots of the A tile
   constexpr int EA = (A4 + kThreads - 1) / kThreads;   // slots per thread
@@ -950,18 +1172,22 @@ double list_makespan(long F, double L, long R, double d, long slots) {
 }
 
 constexpr double kSustainedTflops = 130.0;   // chip-wide fp32 MFMA rate of the GEMM body, all slots busy
+constexpr double kSustainedTflopsBf16 = 300.0;   // the bf16-LDS body (conv_body_bf16), gather-bound
 
 ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {
   ConvPlan pl{};
   conv_tile(M, &pl.bm, &pl.bn);
   pl.gx = (N + pl.bn - 1) / pl.bn;
   pl.gy = (M + pl.bm - 1) / pl.bm;
-  const int kt_total = ((Ck + BK - 1) / BK) * T;
+  // bf16 kernels take K-steps of BKB = two fp32 steps (conv_body_bf16)
+  const int kt_total = bf16 ? (((Ck + BK - 1) / BK) * T + 1) / 2 : ((Ck + BK - 1) / BK) * T;
+  const int bk = bf16 ? BKB : BK;
+  const double rate = bf16 ? kSustainedTflopsBf16 : kSustainedTflops;
   const long tiles = (long)pl.gx * pl.gy;
   // slot-level model (blocks run in rounds of occupancy x CUs); the CU-level "fluid" model was
   // measured 7 % slower over the iteration (it under-splits: a lone block does not fill its CU)
   const long slots = (long)conv_occupancy(pl.bm, pl.bn, mode, bscale, bf16) * num_cus();
-  const double t_k = 2.0 * pl.bm * pl.bn * BK / (kSustainedTflops * 1e12 / slots) * 1e6;   // us per K-step
+  const double t_k = 2.0 * pl.bm * pl.bn * bk / (rate * 1e12 / slots) * 1e6;   // us per K-step
   const double ovh = 1.0 / t_k;           // ~1 us per block of prologue / epilogue, in K-steps
   auto cost = [&](int nf, int S, int* per_out) {
     const int per = (kt_total + S - 1) / S;

@@ -128,7 +128,7 @@ class FlopCounter:
     algo_flops = 0
     flops_bf16 = 0
     launches = 0
-    record = None          # optional list receiving (op, geo, has_xscale, has_yscale)
+    record = None          # optional list receiving (op, geo, has_xscale, has_yscale, math)
 
     @staticmethod
     def algorithmic(geo: "Geo") -> int:
@@ -152,7 +152,7 @@ class FlopCounter:
     @classmethod
     def add(cls, geo: "Geo", op: str = "", xs=False, ys=False):
         if cls.record is not None:
-            cls.record.append((op, geo, xs, ys))
+            cls.record.append((op, geo, xs, ys, "bf16" if _MATH[0] == _lib.MATH_BF16 else "fp32"))
         if cls.enabled:
             f = cls.issued(geo, op)
             cls.flops += f

@@ -206,7 +206,7 @@ def gemm_census(dev, rec, top=8):
     cnt = collections.Counter(rec)
     rows = []
     s = torch.cuda.current_stream()
-    for (op, g, xs, ys), n in cnt.items():
+    for (op, g, xs, ys, math), n in cnt.items():
         xin = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
         yout = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
         w = torch.nn.Parameter(torch.randn((g.Cin, g.Cout, g.K, g.K) if g.transposed else (g.Cout, g.Cin, g.K, g.K),
@@ -220,7 +220,7 @@ def gemm_census(dev, rec, top=8):
             f = lambda: ops._conv_dgrad(g, yout, w, sgy, 1.0)
         else:
             f = lambda: ops._conv_wgrad(g, xin, yout, sx, sy, 1.0)
-        with torch.no_grad():
+        with torch.no_grad(), ops.math_mode(math):
             f()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
@@ -230,7 +230,7 @@ def gemm_census(dev, rec, top=8):
             torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / 5e3
         flop = ops.FlopCounter.algorithmic(g)
-        rows.append((n * t, n, t, flop, op, g, xs or ys))
+        rows.append((n * t, n, t, flop, op, g, xs or ys, math))
         del xin, yout, w, sx, sy
     rows.sort(key=lambda r: -r[0])
     tot_t = sum(r[0] for r in rows)
@@ -240,13 +240,17 @@ def gemm_census(dev, rec, top=8):
     def shape(r):
         g = r[5]
         return (f"{r[4]} B={g.B} {g.Cin}->{g.Cout} {g.H}x{g.W}->{g.OH}x{g.OW} k{g.K} s{g.stride}"
-                f"{' T' if g.transposed else ''}{' scaled' if r[6] else ''}")
+                f"{' T' if g.transposed else ''}{' scaled' if r[6] else ''}{' bf16' if r[7] == 'bf16' else ''}")
+
+    def peak(r):
+        return BF16_MFMA_PEAK_TFLOPS if r[7] == "bf16" else FP32_MFMA_PEAK_TFLOPS
     return {"distinct_shapes": len(rows), "launches_per_iter": sum(r[1] for r in rows),
-            "est_gemm_s_per_iter": tot_t, "gemm_tflops": tf, "gemm_frac": tf / FP32_MFMA_PEAK_TFLOPS,
+            "est_gemm_s_per_iter": tot_t, "gemm_tflops": tf,
+            "gemm_frac": sum(r[1] * r[3] / (peak(r) * 1e12) for r in rows) / tot_t,
             "method": "every distinct conv GEMM of one iteration timed in isolation (HIP events, 5 launches); "
                       "algorithmic FLOPs / (count x time); includes each op's split-K reduce / fold launches",
             "top": [{"shape": shape(r), "count": r[1], "us": 1e6 * r[2], "tflops": r[3] / r[2] / 1e12,
-                     "frac": r[3] / r[2] / 1e12 / FP32_MFMA_PEAK_TFLOPS, "share": r[0] / tot_t} for r in rows[:top]]}
+                     "frac": r[3] / r[2] / 1e12 / peak(r), "share": r[0] / tot_t} for r in rows[:top]]}
 
 
 CONFIGS = {
