@@ -40,7 +40,7 @@ def main():
     torch.cuda.empty_cache()
     cnt = collections.Counter(rec)
     rows = []
-    for (op, g, xs, ys), n in cnt.items():
+    for (op, g, xs, ys, _math), n in cnt.items():
         xin = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
         yout = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
         wshape = (g.Cin, g.Cout, g.K, g.K) if g.transposed else (g.Cout, g.Cin, g.K, g.K)

@@ -54,7 +54,7 @@ if len(sys.argv) > 2 and sys.argv[2] == "census":
     ops.FlopCounter.record = None
     cnt = collections.Counter(rec)
     rows = []
-    for (op, geo, xs, ys), n in cnt.items():
+    for (op, geo, xs, ys, _math), n in cnt.items():
         xin = torch.randn(geo.Cin, geo.B, geo.H, geo.W, device=dev)
         w = torch.randn((geo.Cin, geo.Cout, geo.K, geo.K) if geo.transposed else (geo.Cout, geo.Cin, geo.K, geo.K),
                         device=dev)
