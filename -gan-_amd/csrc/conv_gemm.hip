@@ -1003,6 +1003,10 @@ int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
+int linear_enabled() {   // GANAMD_LINEAR=0: linears through the tiled conv GEMM (A/B)
+  static const int v = env_int("GANAMD_LINEAR", 1);
+  return v;
+}
 int splitk_enabled() {   // GANAMD_SPLITK=0 disables split-K (experiments)
   static const int v = env_int("GANAMD_SPLITK", 1);
   return v;
@@ -1355,6 +1359,101 @@ hipError_t dispatch_conv_mode(const ConvArgs& p, const ConvPlan& pl, float* slab
   }
 }
 
+
+// ---- skinny GEMM for the linears ------------------------------------------------------------
+// EqualizedLinear / nn.Linear on [features][batch] (a 1x1 conv at H = W = 1): M = out features,
+// N = batch (64 .. 384), K = in features.  The tiled conv GEMM spends most of such a launch on one
+// block's serial K loop (or on split-K slabs and a reduce launch): ~16-40 us for a few MFLOP.
+// Here a block owns 32 rows x 128 columns; its 4 waves split K four ways, each streams its quarter
+// straight from global memory into registers (packed A rows: 8 consecutive k per lane; X: one
+// 128-byte line per half-wave per k) two 16-k chunks ahead, and the partial tiles are summed
+// through LDS before the conv epilogue (alpha, scale, bias, PReLU).  No slab, no second launch.
+constexpr int LBM = 32, LBN = 128;
+
+__global__ __launch_bounds__(256) void linear_gemm_kernel(ConvArgs p) {
+  __shared__ __attribute__((aligned(16))) float red[4][LBM * LBN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * LBM, n0 = blockIdx.y * LBN;
+  const int nch = p.Ckp / 16;                                  // 16-k chunks
+  const int c0 = wave * nch / 4, c1 = (wave + 1) * nch / 4;    // this wave's share of K
+  const rsrc_t ra = make_rsrc(p.w, p.w_bytes);
+  const rsrc_t rx = make_rsrc(p.g.src, p.g.src_bytes());
+  const int N = p.N;
+  const bool row_ok = m0 + r < p.M;
+  struct Chunk {
+    f32x4 a0, a1;
+    float b[8][4];
+  };
+  auto load = [&](int c, Chunk& C) {
+    const int ka = c * 16 + 8 * h;
+    const int aoff = row_ok ? 4 * ((m0 + r) * p.Ckp + ka) : kOOB;
+    C.a0 = bload4(ra, aoff);
+    C.a1 = bload4(ra, row_ok ? aoff + 16 : kOOB);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = ka + s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + 32 * j + r;
+        C.b[s][j] = bload(rx, (k < p.Ck && n < N) ? 4 * (k * N + n) : kOOB);
+      }
+    }
+  };
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  auto mma = [&](const Chunk& C) {
+    const float a[8] = {C.a0[0], C.a0[1], C.a0[2], C.a0[3], C.a1[0], C.a1[1], C.a1[2], C.a1[3]};
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], C.b[s][j], acc[j], 0, 0, 0);
+  };
+  Chunk x0, x1;
+  int c = c0;
+  if (c < c1) load(c, x0);
+  for (; c + 1 < c1; c += 2) {
+    load(c + 1, x1);
+    mma(x0);
+    if (c + 2 < c1) load(c + 2, x0);
+    mma(x1);
+  }
+  if (c < c1) mma(x0);
+  // partial tiles of the 4 waves -> LDS -> summed, epilogue, coalesced stores
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[wave][((e & 3) + 8 * (e >> 2) + 4 * h) * LBN + 32 * j + r] = acc[j][e];
+  __syncthreads();
+  for (int idx = tid; idx < LBM * LBN; idx += 256) {
+    const int row = idx / LBN, col = idx - row * LBN;
+    const int m = m0 + row, n = n0 + col;
+    if (m >= p.M || n >= N) continue;
+    float v = p.alpha * (red[0][idx] + red[1][idx] + red[2][idx] + red[3][idx]);
+    if (p.oscale) v *= p.oscale[m * p.g.B + n / p.ohw];
+    if (p.bias) v += p.bias[m];
+    if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + n];
+    if (p.act) v = v > 0.f ? v : p.act[m] * v;
+    p.y[(long)m * p.ldy + n] = v;
+  }
+}
+
+// The linear path: 1x1, 1x1 maps, unmodulated, fp32, and small enough that the K loop of one
+// block does not dominate (above ~4 M weights the tiled GEMM's split-K wins).
+bool linear_ok(const ConvArgs& p) {
+  const Gather& g = p.g;
+  return p.T == 1 && g.H == 1 && g.W == 1 && g.OH == 1 && g.OW == 1 && !g.scale && !p.bf16 && p.ldy == p.N &&
+         (long)p.M * p.Ck <= (4L << 20) && linear_enabled();
+}
+
+hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
+  hipLaunchKernelGGL(linear_gemm_kernel, dim3((p.M + LBM - 1) / LBM, (p.N + LBN - 1) / LBN), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
 // p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
 // GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
@@ -1368,6 +1467,7 @@ hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab,
     p.w = packed;
   }
   p.w_bytes = 4 * mpad * p.T * p.Ckp;
+  if (linear_ok(p)) return launch_linear(p, st);
   const bool s = p.g.scale != nullptr;
   return p.bf16 ? dispatch_conv_mode<true>(p, pl, slab, st, s) : dispatch_conv_mode<false>(p, pl, slab, st, s);
 }

@@ -234,6 +234,14 @@ def gemm_census(dev, rec, top=8):
         del xin, yout, w, sx, sy
     rows.sort(key=lambda r: -r[0])
     tot_t = sum(r[0] for r in rows)
+    if os.environ.get("GANAMD_CENSUS_OUT"):         # full per-shape table (profiles/)
+        with open(os.environ["GANAMD_CENSUS_OUT"], "w") as f:
+            f.write(f"{'share':>6} {'n':>5} {'us':>9} {'TF/s':>7}  op     B  Cin  H   W  Cout OH  OW k s p T sc math\n")
+            for r in rows:
+                g = r[5]
+                f.write(f"{100 * r[0] / tot_t:6.2f} {r[1]:5d} {1e6 * r[2]:9.1f} {r[3] / r[2] / 1e12:7.2f}  {r[4]:5s} "
+                        f"{g.B:3d} {g.Cin:4d} {g.H:3d} {g.W:3d} {g.Cout:4d} {g.OH:3d} {g.OW:3d} {g.K} {g.stride} {g.pad} "
+                        f"{int(g.transposed)} {int(bool(r[6]))} {r[7]}\n")
     tot_f = sum(r[1] * r[3] for r in rows)
     tf = tot_f / tot_t / 1e12
 

@@ -121,7 +121,8 @@ def test_conv_transpose(ops, case):
     assert rel(nc(xa.grad), gx) < 1e-4 and rel(wa.grad, gw) < 1e-4 and rel(ba.grad, gb) < 1e-4
 
 
-@pytest.mark.parametrize("B,cin,cout", [(4, 256, 256), (64, 4100, 4100), (8, 4100, 1), (64, 256, 3072)])
+@pytest.mark.parametrize("B,cin,cout", [(4, 256, 256), (64, 4100, 4100), (8, 4100, 1), (64, 256, 3072), (128, 192, 192),
+                                        (384, 96, 48), (64, 1025, 1025), (192, 3, 70)])
 def test_linear(ops, B, cin, cout):
     g = torch.Generator().manual_seed(B + cin)
     x = torch.randn(B, cin, generator=g, dtype=torch.float64, requires_grad=True)
