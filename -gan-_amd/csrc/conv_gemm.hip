@@ -1368,41 +1368,46 @@ hipError_t dispatch_conv_mode(const ConvArgs& p, const ConvPlan& pl, float* slab
 // straight from global memory into registers (packed A rows: 8 consecutive k per lane; X: one
 // 128-byte line per half-wave per k) two 16-k chunks ahead, and the partial tiles are summed
 // through LDS before the conv epilogue (alpha, scale, bias, PReLU).  No slab, no second launch.
-constexpr int LBM = 32, LBN = 128;
+constexpr int LBM = 32;
 
-__global__ __launch_bounds__(256) void linear_gemm_kernel(ConvArgs p) {
-  __shared__ __attribute__((aligned(16))) float red[4][LBM * LBN];
+// JT: 32-column MFMA tiles per block (2: N <= 64, 4: 128 columns); NW waves split K; chunks of 16 k
+// are loaded four at a time (four in flight per wave) before their MFMAs.
+template <int JT, int NW>
+__global__ __launch_bounds__(64 * NW) void linear_gemm_kernel(ConvArgs p) {
+  constexpr int LBN = 32 * JT;
+  __shared__ __attribute__((aligned(16))) float red[NW][LBM * LBN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int m0 = blockIdx.x * LBM, n0 = blockIdx.y * LBN;
-  const int nch = p.Ckp / 16;                                  // 16-k chunks
-  const int c0 = wave * nch / 4, c1 = (wave + 1) * nch / 4;    // this wave's share of K
+  const int nch = p.Ckp / 16;                                    // 16-k chunks
+  const int c0 = wave * nch / NW, c1 = (wave + 1) * nch / NW;    // this wave's share of K
   const rsrc_t ra = make_rsrc(p.w, p.w_bytes);
   const rsrc_t rx = make_rsrc(p.g.src, p.g.src_bytes());
   const int N = p.N;
   const bool row_ok = m0 + r < p.M;
   struct Chunk {
     f32x4 a0, a1;
-    float b[8][4];
+    float b[8][JT];
   };
   auto load = [&](int c, Chunk& C) {
+    const bool ok = c < c1;
     const int ka = c * 16 + 8 * h;
-    const int aoff = row_ok ? 4 * ((m0 + r) * p.Ckp + ka) : kOOB;
+    const int aoff = (row_ok && ok) ? 4 * ((m0 + r) * p.Ckp + ka) : kOOB;
     C.a0 = bload4(ra, aoff);
-    C.a1 = bload4(ra, row_ok ? aoff + 16 : kOOB);
+    C.a1 = bload4(ra, aoff == kOOB ? kOOB : aoff + 16);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int k = ka + s;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < JT; ++j) {
         const int n = n0 + 32 * j + r;
-        C.b[s][j] = bload(rx, (k < p.Ck && n < N) ? 4 * (k * N + n) : kOOB);
+        C.b[s][j] = bload(rx, (ok && k < p.Ck && n < N) ? 4 * (k * N + n) : kOOB);
       }
     }
   };
-  f32x16 acc[4];
+  f32x16 acc[JT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < JT; ++j)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
   auto mma = [&](const Chunk& C) {
@@ -1410,29 +1415,33 @@ __global__ __launch_bounds__(256) void linear_gemm_kernel(ConvArgs p) {
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], C.b[s][j], acc[j], 0, 0, 0);
+      for (int j = 0; j < JT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], C.b[s][j], acc[j], 0, 0, 0);
   };
-  Chunk x0, x1;
-  int c = c0;
-  if (c < c1) load(c, x0);
-  for (; c + 1 < c1; c += 2) {
+  for (int c = c0; c < c1; c += 4) {     // chunks past c1 load zeros (OOB), their MFMAs add 0
+    Chunk x0, x1, x2, x3;
+    load(c, x0);
     load(c + 1, x1);
+    load(c + 2, x2);
+    load(c + 3, x3);
     mma(x0);
-    if (c + 2 < c1) load(c + 2, x0);
-    mma(x1);
+    if (c + 1 < c1) mma(x1);
+    if (c + 2 < c1) mma(x2);
+    if (c + 3 < c1) mma(x3);
   }
-  if (c < c1) mma(x0);
-  // partial tiles of the 4 waves -> LDS -> summed, epilogue, coalesced stores
+  // partial tiles of the NW waves -> LDS -> summed, epilogue, coalesced stores
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < JT; ++j)
 #pragma unroll
     for (int e = 0; e < 16; ++e) red[wave][((e & 3) + 8 * (e >> 2) + 4 * h) * LBN + 32 * j + r] = acc[j][e];
   __syncthreads();
-  for (int idx = tid; idx < LBM * LBN; idx += 256) {
+  for (int idx = tid; idx < LBM * LBN; idx += 64 * NW) {
     const int row = idx / LBN, col = idx - row * LBN;
     const int m = m0 + row, n = n0 + col;
     if (m >= p.M || n >= N) continue;
-    float v = p.alpha * (red[0][idx] + red[1][idx] + red[2][idx] + red[3][idx]);
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][idx];
+    v *= p.alpha;
     if (p.oscale) v *= p.oscale[m * p.g.B + n / p.ohw];
     if (p.bias) v += p.bias[m];
     if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + n];
@@ -1450,7 +1459,10 @@ bool linear_ok(const ConvArgs& p) {
 }
 
 hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
-  hipLaunchKernelGGL(linear_gemm_kernel, dim3((p.M + LBM - 1) / LBM, (p.N + LBN - 1) / LBN), dim3(256), 0, st, p);
+  if (p.N <= 64)
+    hipLaunchKernelGGL((linear_gemm_kernel<2, 8>), dim3((p.M + LBM - 1) / LBM, 1), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL((linear_gemm_kernel<4, 4>), dim3((p.M + LBM - 1) / LBM, (p.N + 127) / 128), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 

@@ -51,6 +51,13 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
   return sh[0] + sh[1] + sh[2] + sh[3];
 }
 
+// Per-(row, split) partial of a row reduction.  acc_mode 0: a partial slot (reduce1_kernel folds
+// them); with a single split the partial IS the result and the kernel writes it directly --
+// 1: store, 2: accumulate -- saving the fold launch.
+__device__ __forceinline__ void put_part(float* part, long idx, float v, int acc_mode) {
+  part[idx] = acc_mode == 2 ? part[idx] + v : v;
+}
+
 inline int splits_for(long L) {
   long s = (L + kChunk - 1) / kChunk;
   if (s < 1) s = 1;
@@ -426,7 +433,8 @@ __global__ __launch_bounds__(kNT) void prelu_fwd_vec_kernel(const float* __restr
 // gx (optional) and per-block partials of galpha = sum gy*x over x<=0
 __global__ __launch_bounds__(kNT) void prelu_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
                                                         const float* __restrict__ a, long L, int S,
-                                                        float* __restrict__ gx, float* __restrict__ part) {
+                                                        float* __restrict__ gx, float* __restrict__ part,
+                                                        int acc_mode) {
   __shared__ float sh[4];
   const int c = blockIdx.y, s = blockIdx.x;
   const long per = (L + S - 1) / S;
@@ -470,7 +478,7 @@ __global__ __launch_bounds__(kNT) void prelu_bwd_kernel(const float* __restrict_
   }
   if (part) {
     acc = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[(long)c * S + s] = acc;
+    if (threadIdx.x == 0) put_part(part, (long)c * S + s, acc, acc_mode);
   }
 }
 
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(kNT) void prelu_bwd_bwd_kernel(const float* __restr
                                                             const float* __restrict__ gy, const float* __restrict__ x,
                                                             const float* __restrict__ a, long L, int S,
                                                             float* __restrict__ ggy, float* __restrict__ gx,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part, int acc_mode) {
   __shared__ float sh[4];
   const int c = blockIdx.y, s = blockIdx.x;
   const long per = (L + S - 1) / S;
@@ -503,7 +511,7 @@ __global__ __launch_bounds__(kNT) void prelu_bwd_bwd_kernel(const float* __restr
   }
   if (part) {
     acc = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[(long)c * S + s] = acc;
+    if (threadIdx.x == 0) put_part(part, (long)c * S + s, acc, acc_mode);
   }
 }
 
@@ -517,7 +525,7 @@ __global__ void reduce1_kernel(const float* __restrict__ part, int C, int S, flo
 
 // ---------------------------------------------------------------- row / plane reductions
 __global__ __launch_bounds__(kNT) void row_dot_kernel(const float* __restrict__ a, const float* __restrict__ b, long L,
-                                                      int S, float* __restrict__ part) {
+                                                      int S, float* __restrict__ part, int acc_mode) {
   __shared__ float sh[4];
   const int c = blockIdx.y, s = blockIdx.x;
   const long per = (L + S - 1) / S;
@@ -530,7 +538,7 @@ __global__ __launch_bounds__(kNT) void row_dot_kernel(const float* __restrict__ 
     for (long i = lo + threadIdx.x; i < hi; i += kNT) acc += a[base + i];
   }
   acc = block_sum(acc, sh);
-  if (threadIdx.x == 0) part[(long)c * S + s] = acc;
+  if (threadIdx.x == 0) put_part(part, (long)c * S + s, acc, acc_mode);
 }
 
 // one wave per plane
@@ -781,9 +789,10 @@ int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C,
                      int accumulate, void* workspace, hipStream_t st) {
   if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
   const int S = splits_for(L);
-  float* part = galpha ? static_cast<float*>(workspace) : nullptr;
-  hipLaunchKernelGGL(prelu_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, alpha, L, S, gx, part);
-  if (galpha)
+  float* part = galpha ? (S == 1 ? galpha : static_cast<float*>(workspace)) : nullptr;
+  hipLaunchKernelGGL(prelu_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, alpha, L, S, gx, part,
+                     S == 1 ? 1 + (accumulate != 0) : 0);
+  if (galpha && S > 1)
     hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, accumulate);
   return ok(hipGetLastError());
 }
@@ -792,10 +801,11 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
                          int C, long L, float* ggy, float* gx, float* galpha, void* workspace, hipStream_t st) {
   if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
   const int S = splits_for(L);
-  float* part = galpha ? static_cast<float*>(workspace) : nullptr;
+  float* part = galpha ? (S == 1 ? galpha : static_cast<float*>(workspace)) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, ggx, ggalpha, gy, x, alpha, L, S, ggy, gx,
-                     part);
-  if (galpha) hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, 0);
+                     part, S == 1 ? 1 : 0);
+  if (galpha && S > 1)
+    hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, 0);
   return ok(hipGetLastError());
 }
 
@@ -803,10 +813,10 @@ int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const
                          float* galpha, int accumulate, void* workspace, hipStream_t st) {
   if (!xd || !gy || !x || !alpha || !yd || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
   const int S = splits_for(L);
-  float* part = galpha ? static_cast<float*>(workspace) : nullptr;
+  float* part = galpha ? (S == 1 ? galpha : static_cast<float*>(workspace)) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, xd, nullptr, gy, x, alpha, L, S, yd, nullptr,
-                     part);
-  if (galpha)
+                     part, S == 1 ? 1 + (accumulate != 0) : 0);
+  if (galpha && S > 1)
     hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, galpha, accumulate);
   return ok(hipGetLastError());
 }
@@ -853,8 +863,12 @@ int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, in
                    hipStream_t st) {
   if (!a || !out || !workspace || C <= 0 || L <= 0) return GANAMD_EINVAL;
   const int S = splits_for(L);
+  if (S == 1) {
+    hipLaunchKernelGGL(row_dot_kernel, dim3(S, C), dim3(kNT), 0, st, a, b, L, S, out, 1 + (accumulate != 0));
+    return ok(hipGetLastError());
+  }
   float* part = static_cast<float*>(workspace);
-  hipLaunchKernelGGL(row_dot_kernel, dim3(S, C), dim3(kNT), 0, st, a, b, L, S, part);
+  hipLaunchKernelGGL(row_dot_kernel, dim3(S, C), dim3(kNT), 0, st, a, b, L, S, part, 0);
   hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, C, S, out, accumulate);
   return ok(hipGetLastError());
 }
