@@ -283,33 +283,35 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
 // Element i of a job's GEMM-order output.  ps > 1: the s*s phases of a stride-s transposed conv
 // one after another, phase q = (qh, qw) over its (K/s)^2 taps t' = (a, b) -> kernel tap
 // (kh0 + s*a, kw0 + s*b) with kh0 = (qh + pad) % s (see kPhase).
-__device__ __forceinline__ float pack_elem(const ganamd_pack_job& j, long i) {
-  const int nct = j.Ckp / BK;
-  int T = j.T, q = 0;
+// 32-bit index arithmetic (every job's packed size and weight extent is far below 2^31, checked at
+// job creation; 64-bit divisions per element made the batched repack compute-bound).
+__device__ __forceinline__ float pack_elem(const ganamd_pack_job& j, unsigned i) {
+  const unsigned nct = (unsigned)j.Ckp / BK;
+  unsigned T = (unsigned)j.T, q = 0;
   if (j.ps > 1) {
-    T = j.T / (j.ps * j.ps);
-    const long per = (long)j.Mpad * T * j.Ckp;
-    q = (int)(i / per);
+    T = (unsigned)(j.T / (j.ps * j.ps));
+    const unsigned per = (unsigned)j.Mpad * T * (unsigned)j.Ckp;
+    q = i / per;
     i -= q * per;
   }
-  const int c16 = (int)(i % BK);
-  const long r = i / BK;
-  int t = (int)(r % T);
-  const long r2 = r / T;
-  const int cc = (int)(r2 % nct);
+  const unsigned c16 = i % BK;
+  const unsigned r = i / BK;
+  unsigned t = r % T;
+  const unsigned r2 = r / T;
+  const unsigned cc = r2 % nct;
   const int m = (int)(r2 / nct);
-  const int c = cc * BK + c16;
+  const int c = (int)(cc * BK + c16);
   if (j.ps > 1) {
-    const int kk = j.pk / j.ps, qh = q / j.ps, qw = q - qh * j.ps;
-    const int kh = (qh + j.ppad) % j.ps + j.ps * (t / kk), kw = (qw + j.ppad) % j.ps + j.ps * (t % kk);
-    t = kh * j.pk + kw;
+    const int kk = j.pk / j.ps, qh = (int)q / j.ps, qw = (int)q - qh * j.ps;
+    const int kh = (qh + j.ppad) % j.ps + j.ps * ((int)t / kk), kw = (qw + j.ppad) % j.ps + j.ps * ((int)t % kk);
+    t = (unsigned)(kh * j.pk + kw);
   }
-  return (m < j.M && c < j.Ck) ? j.w[(long)m * j.sm + (long)c * j.sc + (long)t * j.st] : 0.f;
+  return (m < j.M && c < j.Ck) ? j.w[(unsigned)(m * j.sm + c * j.sc) + t * (unsigned)j.st] : 0.f;
 }
 
 __global__ void pack_a_kernel(ganamd_pack_job j) {
-  const long total = (long)j.Mpad * j.T * j.Ckp;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+  const unsigned total = (unsigned)j.Mpad * j.T * j.Ckp;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
     j.out[i] = pack_elem(j, i);
 }
 
@@ -762,9 +764,10 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
     if (jobs[mid].chunk0 <= b) lo = mid; else hi = mid - 1;
   }
   const ganamd_pack_job j = jobs[lo];
-  const long total = (long)j.Mpad * j.T * j.Ckp;
-  const long i0 = (b - j.chunk0) * kPackChunk;
-  for (long i = i0 + threadIdx.x; i < min(total, i0 + kPackChunk); i += 256) j.out[i] = pack_elem(j, i);
+  const unsigned total = (unsigned)j.Mpad * j.T * j.Ckp;
+  const unsigned i0 = (unsigned)(b - j.chunk0) * kPackChunk;
+  const unsigned i1 = min(total, i0 + kPackChunk);
+  for (unsigned i = i0 + threadIdx.x; i < i1; i += 256) j.out[i] = pack_elem(j, i);
 }
 
 // ------------------------------------------------------------------------------------------
