@@ -1034,7 +1034,17 @@ struct Plan {
   int bm, bn, splits, kt_per_split;
 };
 
-int conv_bm(int M) { return M <= 32 ? 32 : M <= 64 ? 64 : M <= 96 ? 96 : 128; }
+// Row tile: the least padded rows per unit of tile efficiency (measured: 96-row tiles ~0.95 and
+// 64-row ~0.9 of the 128-row rate) -- e.g. M = 192 takes two 96-row tiles, not two 128-row ones
+// (256 rows, 25 % empty); a smaller tile has to beat the 128-row one by 5 %.
+int conv_bm(int M) {
+  if (M <= 32) return 32;
+  if (M <= 64) return 64;
+  if (M <= 96) return 96;
+  const double c128 = (M + 127) / 128 * 128.0, c96 = (M + 95) / 96 * 96.0 / 0.95, c64 = (M + 63) / 64 * 64.0 / 0.9;
+  const double bar = 0.95 * c128;   // a smaller tile only for a clear win
+  return (c96 < bar && c96 <= c64) ? 96 : (c64 < bar ? 64 : 128);
+}
 int wide_tiles() {   // GANAMD_WIDE=1: 128 x 256 tiles (2 waves per SIMD) for M > 96 (A/B experiments)
   static const int v = env_int("GANAMD_WIDE", 0);
   return v;
