@@ -127,7 +127,7 @@ class SEBlock_conv(nn.Module):
         t = prelu(c[0](ops.resample(x, "pool5")), c[1].weight)
         t = prelu(c[2](t), c[3].weight)
         z = prelu(self.fcs[0](ops.plane_mean(t)), self.fcs[1].weight)
-        return torch.sigmoid(self.fc_out(z))
+        return ops.sigmoid(self.fc_out(z))
 
 
 class SEBlock_fc(nn.Module):
@@ -143,7 +143,7 @@ class SEBlock_fc(nn.Module):
         f = self.fcs
         z = prelu(f[0](ops.plane_mean(x)), f[1].weight)
         z = prelu(f[2](z), f[3].weight)
-        return torch.sigmoid(self.fc_out(z))
+        return ops.sigmoid(self.fc_out(z))
 
 
 class DiscriminatorBlock(nn.Module):

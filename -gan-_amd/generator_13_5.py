@@ -87,7 +87,7 @@ def _heads(attn, z):
         sub = getattr(attn, f"fc_sub_{i}")
         v = _lin_bn_act(sub[0], sub[1], sub[2], z)
         vecs.append(sub[3](v))
-    return torch.softmax(torch.stack(vecs, 0), dim=0)          # [M, C, B]
+    return ops.softmax_m(torch.stack(vecs, 0))          # [M, C, B], softmax over M
 
 
 class SKAttention_conv(nn.Module):
@@ -354,7 +354,7 @@ class SEBlock_conv(nn.Module):
         t = _conv_bn_act(c[0], c[1], c[2], ops.resample(x, "pool5"))
         t = _conv_bn_act(c[3], c[4], c[5], t)
         z = _lin_bn_act(self.fcs[0], self.fcs[1], self.fcs[2], ops.plane_mean(t))
-        return torch.sigmoid(bn_act(self.fc_out(z), self.fc_bn, None))
+        return ops.sigmoid(bn_act(self.fc_out(z), self.fc_bn, None))
 
 
 class SEBlock_fc(nn.Module):
@@ -373,7 +373,7 @@ class SEBlock_fc(nn.Module):
         f = self.fcs
         z = _lin_bn_act(f[0], f[1], f[2], ops.plane_mean(x))
         z = _lin_bn_act(f[3], f[4], f[5], z)
-        return torch.sigmoid(bn_act(self.fc_out(z), self.fc_bn, None))
+        return ops.sigmoid(bn_act(self.fc_out(z), self.fc_bn, None))
 
 
 class BasicBlock(nn.Module):

@@ -1087,3 +1087,30 @@ class BCELoss(Function):
 
 def bce_loss(p, target):
     return BCELoss.apply(p, target)
+
+
+class SoftmaxM(Function):
+    """softmax over the M branch axis of x[M][P] (the SK attention heads, generator_13_5.py:88,131:
+    softmax(dim=1) of [B, M, C, 1, 1]); backward gx = y (gy - <y, gy>_M)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x)
+        M = x.shape[0]
+        y = torch.empty_like(x)
+        check(LIB.ganamd_softmax_m(M, ptr(x), x.numel() // M, ptr(y), stream()), "softmax_m")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        gy = _c(gy)
+        M = y.shape[0]
+        gx = torch.empty_like(y)
+        check(LIB.ganamd_softmax_m_bwd(M, ptr(y), ptr(gy), y.numel() // M, ptr(gx), stream()), "softmax_m_bwd")
+        return gx
+
+
+def softmax_m(x):
+    return SoftmaxM.apply(x)
