@@ -32,6 +32,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/ganamd.h"
 
@@ -327,6 +328,27 @@ constexpr int BKB = 32;        // bf16 K-step
 constexpr int LDB = BKB + 8;   // LDS row stride (bf16 elements): 80 B, 16-B aligned, ds_read_b128 conflict-free
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// One 16-deep K-step of bf16 MFMAs for a wave over bf16 LDS tiles (rows of LDB elements):
+// lane (r, h) reads the 8 k of its row with one ds_read_b128.
+template <class C>
+__device__ __forceinline__ void mfma_tile_lds_bf16(const unsigned short* __restrict__ As,
+                                                   const unsigned short* __restrict__ Bs,
+                                                   f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0) {
+  const int r = lane & 31, h = lane >> 5;
+  bf16x8 av[C::TM], bv[C::TN];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+    av[i] = *reinterpret_cast<const bf16x8*>(&As[((wm * C::TM + i) * 32 + r) * LDB + k0 + 8 * h]);
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j)
+    bv[j] = *reinterpret_cast<const bf16x8*>(&Bs[((wn * C::TN + j) * 32 + r) * LDB + k0 + 8 * h]);
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+}
 
 __device__ __forceinline__ u16x8 to_bf16x8(const float* v) {
   bf16x8 b;
@@ -781,8 +803,12 @@ void wgrad_gemm_kernel(WgradArgs p) {
   constexpr int EA = (A4 + kThreads - 1) / kThreads;
   constexpr int EB = BKW * BN / kThreads;
   constexpr int RSTEP = kThreads / BKW;
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDKW];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDKW];
+  // bf16 math stages the tiles in LDS as bf16 (80-byte rows, one ds_read_b128 per fragment);
+  // fp32 keeps fp32 rows of LDKW floats
+  using LT = typename std::conditional<BF16, unsigned short, float>::type;
+  constexpr int LDW = BF16 ? LDB : LDKW;
+  __shared__ __attribute__((aligned(16))) LT As[2][BM * LDW];
+  __shared__ __attribute__((aligned(16))) LT Bs[2][BN * LDW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -882,13 +908,26 @@ void wgrad_gemm_kernel(WgradArgs p) {
       if (slot < A4) {
         f32x4 v = ra[e];
         if (SCALED) v *= rsa[e];
-        float* d = &As[buf][(slot / (BKW / 4)) * LDKW + 4 * (slot % (BKW / 4))];
-        *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
-        *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
+        LT* d = &As[buf][(slot / (BKW / 4)) * LDW + 4 * (slot % (BKW / 4))];
+        if constexpr (BF16) {
+          bf16x4 b;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) b[q] = (__bf16)v[q];
+          *reinterpret_cast<bf16x4*>(d) = b;
+        } else {
+          *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
+          *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
+        }
       }
     }
 #pragma unroll
-    for (int e = 0; e < EB; ++e) Bs[buf][(tr + e * RSTEP) * LDKW + tk] = SCALED ? rb[e] * rsb[e] : rb[e];
+    for (int e = 0; e < EB; ++e) {
+      const float v = SCALED ? rb[e] * rsb[e] : rb[e];
+      if constexpr (BF16)
+        Bs[buf][(tr + e * RSTEP) * LDW + tk] = __builtin_bit_cast(unsigned short, (__bf16)v);
+      else
+        Bs[buf][(tr + e * RSTEP) * LDW + tk] = v;
+    }
   };
 
   f32x16 acc[C::TM][C::TN];
@@ -902,7 +941,12 @@ void wgrad_gemm_kernel(WgradArgs p) {
     const bool more = kt + 1 < kt1;
     if (more) gload(kt + 1);
 #pragma unroll
-    for (int k0 = 0; k0 < BKW; k0 += 16) mfma_tile<C, LDKW, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
+    for (int k0 = 0; k0 < BKW; k0 += 16) {
+      if constexpr (BF16)
+        mfma_tile_lds_bf16<C>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
+      else
+        mfma_tile<C, LDKW, false>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
+    }
     if (more) sstore(buf ^ 1);
     __syncthreads();
   }
