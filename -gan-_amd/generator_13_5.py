@@ -188,6 +188,8 @@ class SKConv(nn.Module):
         self.sk_attention = (SKAttention_conv if image_size > 4 else SKAttention_fc)(out_planes, m)
 
     def forward(self, x):
+        # (the k3 / k5 branches inside one of ResnetInit's parallel StyleBlocks would nest stream
+        # forks; nested forks crash HIP graph capture here, so only ResnetInit branches)
         feas = [_conv_bn_act(getattr(self, f"conv_{i}"), getattr(self, f"BatchNorm_{i}"),
                              getattr(self, f"nonlinear_{i}"), x) for i in range(self.M)]
         return _mix(feas, self.sk_attention(feas))
@@ -327,10 +329,18 @@ class ResnetInit(nn.Module):
 
     def forward(self, x, w):
         x_res, x_tr = x
-        r_r = self.residual(x_res, w)
-        r_t = self.residual_across(x_res, w)
-        t_t = self.transient(x_tr, w)
-        t_r = self.transient_across(x_tr, w)
+        # the four StyleBlocks are independent: on a GPU each runs on its own HIP stream (their
+        # hundreds of small, launch-bound kernels overlap; a captured graph keeps the branches),
+        # issued in the reference's order so the noise draws keep theirs
+        with ops.Branches(x_res.device, 4) as br:
+            with br[0]:
+                r_r = self.residual(x_res, w)
+            with br[1]:
+                r_t = self.residual_across(x_res, w)
+            with br[2]:
+                t_t = self.transient(x_tr, w)
+            with br[3]:
+                t_r = self.transient_across(x_tr, w)
         return (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
                 ops.add_prelu(r_t, t_t, self.activation_transient.weight))
 

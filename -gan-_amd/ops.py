@@ -14,6 +14,7 @@ Generator-only operators (fused BatchNorm+PReLU, the modulated conv) are first-o
 from __future__ import annotations
 
 import contextlib
+import os
 
 from dataclasses import dataclass
 
@@ -1114,3 +1115,52 @@ class SoftmaxM(Function):
 
 def softmax_m(x):
     return SoftmaxM.apply(x)
+
+
+# ------------------------------------------------------------------------------------------
+# independent branches on their own HIP streams
+# ------------------------------------------------------------------------------------------
+
+BRANCH_STREAMS = [os.environ.get("GANAMD_BRANCHES", "1") != "0"]   # A/B: GANAMD_BRANCHES=0 runs branches inline
+_STREAM_POOL: dict = {}
+
+
+class Branches:
+    """``with Branches(dev, n) as br: with br[i]: ...`` -- each branch body runs on its own pooled
+    HIP stream, forked from the current stream on entry and joined back into it on exit (a captured
+    graph gets parallel branches).  Nested branch sets take streams from a pool of their own
+    nesting depth.  Tensors a branch allocates are consumed on the current stream only after the
+    join, and every later branch forks after that consumer, so the caching allocator never hands a
+    branch's memory to work that could overlap its readers.  On the CPU, or with BRANCH_STREAMS[0]
+    False, the bodies run inline."""
+
+    _depth = [0]
+
+    def __init__(self, device, n):
+        dev = torch.device(device)
+        self.on = BRANCH_STREAMS[0] and dev.type == "cuda" and n > 1
+        self.n = n
+        if self.on:
+            key = (dev.index if dev.index is not None else torch.cuda.current_device(), Branches._depth[0])
+            pool = _STREAM_POOL.setdefault(key, [])
+            while len(pool) < n:
+                pool.append(torch.cuda.Stream(device=dev))
+            self.streams = pool[:n]
+
+    def __enter__(self):
+        if self.on:
+            Branches._depth[0] += 1
+            self.main = torch.cuda.current_stream()
+            for s in self.streams:
+                s.wait_stream(self.main)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            Branches._depth[0] -= 1
+            for s in self.streams:
+                self.main.wait_stream(s)
+        return False
+
+    def __getitem__(self, i):
+        return torch.cuda.stream(self.streams[i]) if self.on else contextlib.nullcontext()
