@@ -378,12 +378,16 @@ def main():
                 fn()
             return g
 
-        if world > 1 and args.config == "wgangp" and not args.no_overlap:
-            # Data-parallel critic steps with the overlap SURVEY.md §8(e)(2) allows: the next
-            # critic step's fake batch (no-grad G forward, 41 % of a critic step's FLOPs) depends
-            # on G's weights only, so it runs on a second stream while this step's RCCL
-            # all-reduce of the critic gradient and the AdamW update run on the main stream.
-            # The fake-batch graph has its own memory pool (it replays concurrently with others).
+        if args.config == "wgangp" and not args.no_overlap:
+            # Critic steps with the overlap SURVEY.md §8(e)(2) allows: the next critic step's fake
+            # batch (no-grad G forward, 41 % of a critic step's FLOPs) depends on G's weights
+            # only -- G does not change during the n_critic steps -- so it runs on a second
+            # stream while this step's critic passes, gradient penalty, (N > 1: RCCL all-reduce)
+            # and AdamW run on the main stream; the generator's many small launch-bound kernels
+            # then share the GPU with the critic's large GEMMs.  The work per iteration is
+            # unchanged (5 generator forwards, 5 critic steps, 1 generator step); only the z /
+            # noise draws of the next step come before this step's eps draw.  The fake-batch
+            # graph has its own memory pool (it replays concurrently with others).
             fake = {}
 
             def gfwd():
@@ -401,22 +405,38 @@ def main():
             side = torch.cuda.Stream()
             torch.cuda.synchronize()
             if rank == 0:
-                print("[bench] captured the pipelined data-parallel graphs", file=sys.stderr, flush=True)
+                print("[bench] captured the pipelined critic-step graphs", file=sys.stderr, flush=True)
+
+            fake_next = {}
+
+            def gfwd_next():
+                fake_next["x"] = tr.generate_fake(B)
+
+            # double-buffered fake batch: the side stream writes buffer (i+1)%2 while the critic
+            # reads buffer i%2 (a second captured copy of the generator forward, its own pool)
+            g_fwd2 = capture(gfwd_next, torch.cuda.graph_pool_handle())
+            g_fwd2.replay()
+            g_crit2 = capture(lambda: tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B,
+                                                                gen_imgs=fake_next["x"]))
+            fwd_graphs, crit_graphs = (g_fwd, g_fwd2), (g_crit, g_crit2)
+            torch.cuda.synchronize()
 
             def step():
                 cur = torch.cuda.current_stream()
-                g_fwd.replay()                   # G changed in the previous generator step
+                fwd_graphs[0].replay()           # G changed in the previous generator step
                 for i in range(N_CRITIC):
-                    g_crit.replay()
-                    if i + 1 < N_CRITIC:
-                        side.wait_stream(cur)    # this step's critic has read the fake batch
+                    if i + 1 < N_CRITIC:         # the next step's fake batch, concurrently
+                        side.wait_stream(cur)    # (its buffer was last read two steps ago)
                         with torch.cuda.stream(side):
-                            g_fwd.replay()
-                    allreduce_mean_(tr.optimizer_D.flat.grad)
+                            fwd_graphs[(i + 1) % 2].replay()
+                    crit_graphs[i % 2].replay()
+                    if world > 1:
+                        allreduce_mean_(tr.optimizer_D.flat.grad)
                     g_dstep.replay()
                     cur.wait_stream(side)
                 g_gen.replay()
-                allreduce_mean_(tr.optimizer_G.flat.grad)
+                if world > 1:
+                    allreduce_mean_(tr.optimizer_G.flat.grad)
                 g_gstep.replay()
         else:
             for key, bwd, opt, _ in phases:
