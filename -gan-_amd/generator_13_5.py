@@ -241,9 +241,7 @@ class Conv2dWeightModulate(nn.Module):
             d = ops.demod(s, self.weight.weights, self.weight.scale)
         if not torch.is_grad_enabled():
             return ops.modconv_fused(x, s, d, self.weight.weights, geo, self.weight.scale, noise, noise_scale, act)
-        y = ops.ModConv.apply(x, s, d, self.weight.weights, geo, self.weight.scale)
-        if noise is not None:
-            y = y + noise_scale[:, None, None, None] * noise
+        y = ops.ModConv.apply(x, s, d, self.weight.weights, geo, self.weight.scale, noise_scale, noise)
         return y if act is None else prelu(y, act)
 
 

@@ -744,19 +744,35 @@ class ModConv(Function):
     """
 
     @staticmethod
-    def forward(ctx, x, s, d, w, geo, c):
+    def forward(ctx, x, s, d, w, geo, c, noise_scale=None, noise=None):
+        """``noise_scale``/``noise``: the StyleConv noise term ``+ noise_scale[co] * noise`` fused in
+        the GEMM epilogue (generator_13_5.py:265); its gradients come from one plane reduction."""
         ctx.w_arg = w
         x, s, d, w = _c(x), _c(s), _c(d), _c(w)
-        y = _conv_fwd(geo, x, w, None, s, d, c)
-        ctx.save_for_backward(x, s, d, w, y)
-        ctx.geo, ctx.c = geo, c
+        if noise is None:
+            y = _conv_fwd(geo, x, w, None, s, d, c)
+            ctx.save_for_backward(x, s, d, w, y)
+        else:
+            noise = _c(noise)
+            y = _conv_fwd_ex(geo, x, w, s, d, c, noise, _c(noise_scale))
+            ctx.save_for_backward(x, s, d, w, y, noise_scale, noise)
+        ctx.geo, ctx.c, ctx.noisy = geo, c, noise is not None
         return y
 
     @staticmethod
     @once_differentiable
     def backward(ctx, gy):
-        x, s, d, w, y = ctx.saved_tensors
+        if ctx.noisy:
+            x, s, d, w, y, ns, noise = ctx.saved_tensors
+        else:
+            (x, s, d, w, y), ns, noise = ctx.saved_tensors, None, None
         geo, c = ctx.geo, ctx.c
+        gns = None
+        pdn = None
+        if noise is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[6]):
+            pdn = plane_dot(gy, noise)                      # [C, B]: sum_hw gy * noise
+            if ctx.needs_input_grad[6]:
+                gns = pdn.sum(1)
         gy = _c(gy)
         gx = gs = gd = gw = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
@@ -768,14 +784,17 @@ class ModConv(Function):
             check(LIB.ganamd_mix_bwd(1, ptr(x), None, None, None, ptr(s), P, HW, ptr(gxs), ptr(gx), None, None, None,
                                      ptr(gs), stream()), "mix_bwd")
         if ctx.needs_input_grad[2]:
-            gd = plane_dot(gy, y) / d                       # y = d * conv  =>  dL/dd = sum gy*conv
+            pdy = plane_dot(gy, y)                          # y = d * conv (+ ns * noise)
+            if pdn is not None:
+                pdy = pdy - ns[:, None] * pdn
+            gd = pdy / d                                    # dL/dd = sum gy * conv
         if ctx.needs_input_grad[3]:
             tgt = flat_grad(ctx.w_arg)
             if tgt is not None:
                 _conv_wgrad(geo, x, gy, s, d, c, out=tgt, accumulate=True)
             else:
                 gw = _conv_wgrad(geo, x, gy, s, d, c)
-        return gx, gs, gd, gw, None, None
+        return gx, gs, gd, gw, None, None, gns, None
 
 
 def demod(s, w, c, eps=1e-8):
