@@ -778,6 +778,33 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
 // kPackChunk consecutive elements of that job's GEMM-order output.
 constexpr int kPackChunk = 4096;
 
+// Jobs whose channel stride is the large one (the dgrad-order, scatter-dgrad and ConvT copies:
+// A(m, t, c) = S[c][m*T + t], rows r = m*T + t contiguous) pack as tiled transposes: a block reads
+// 16 channel rows x (kPackRows(T) * T) contiguous floats into LDS and writes kPackRows(T) output
+// rows of T*16 contiguous floats -- coalesced on both sides (the element-wise map reads them with a
+// stride of Cin*T floats).
+__host__ __device__ inline bool pack_transposed(const ganamd_pack_job& j) {
+  return j.ps <= 1 && j.st == 1 && j.sm == j.T && j.sc > j.sm;
+}
+__host__ __device__ inline int pack_rows(int T) { return T >= 256 ? 1 : 256 / T; }
+
+__device__ void pack_tile(const ganamd_pack_job& j, long tile, float* lds) {
+  const int T = j.T, R = pack_rows(T), nct = j.Ckp / BK;
+  const int cc = (int)(tile % nct), m0 = (int)(tile / nct) * R;
+  const int rows = min(R, j.Mpad - m0);
+  const int span = rows * T;                                  // contiguous floats per channel row
+  for (int idx = threadIdx.x; idx < BK * span; idx += blockDim.x) {
+    const int c16 = idx / span, r = idx - c16 * span;
+    const int c = cc * BK + c16, m = m0 + r / T;
+    lds[c16 * (R * T + 1) + r] = (c < j.Ck && m < j.M) ? j.w[(long)c * j.sc + (long)m0 * T + r] : 0.f;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < span * BK; idx += blockDim.x) {
+    const int mr = idx / (T * BK), rem = idx - mr * T * BK, t = rem / BK, c16 = rem - t * BK;
+    j.out[(((long)(m0 + mr) * nct + cc) * T + t) * BK + c16] = lds[c16 * (R * T + 1) + mr * T + t];
+  }
+}
+
 __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* __restrict__ jobs, int n_jobs) {
   const long b = blockIdx.x;
   int lo = 0, hi = n_jobs - 1;
@@ -786,6 +813,11 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
     if (jobs[mid].chunk0 <= b) lo = mid; else hi = mid - 1;
   }
   const ganamd_pack_job j = jobs[lo];
+  if (pack_transposed(j)) {
+    __shared__ float lds[BK * (256 + 1)];
+    pack_tile(j, b - j.chunk0, lds);
+    return;
+  }
   const unsigned total = (unsigned)j.Mpad * j.T * j.Ckp;
   const unsigned i0 = (unsigned)(b - j.chunk0) * kPackChunk;
   const unsigned i1 = min(total, i0 + kPackChunk);
@@ -1751,6 +1783,8 @@ int ganamd_conv_pack_job(const ganamd_conv_desc* d, int op, const float* w, floa
 
 int64_t ganamd_pack_job_chunks(const ganamd_pack_job* job) {
   if (!job) return 0;
+  if (pack_transposed(*job))   // one tile = kPackRows(T) output rows of one channel chunk
+    return (long)(job->Ckp / BK) * ((job->Mpad + pack_rows(job->T) - 1) / pack_rows(job->T));
   const long total = (long)job->Mpad * job->T * job->Ckp;
   return (total + kPackChunk - 1) / kPackChunk;
 }
