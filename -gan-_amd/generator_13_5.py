@@ -267,6 +267,13 @@ class StyleConv(nn.Module):
         return self.conv(x, w, noise, self.scale_noise if self.use_noise else None, act)
 
 
+import os as _os
+
+# stream-branch placement (A/B): ResnetInit's four StyleBlocks (default) or the SK k3/k5 branches
+RESNET_BRANCHES = [_os.environ.get("GANAMD_RESNET_BRANCHES", "1") != "0"]
+SK_BRANCHES = [_os.environ.get("GANAMD_SK_BRANCHES", "0") != "0"]
+
+
 class SKStyleConv(nn.Module):
     """k3 || k5 StyleConv + noise + PReLU, SK-mixed (generator_13_5.py:269-295)."""
 
@@ -281,7 +288,14 @@ class SKStyleConv(nn.Module):
         self.sk_attention = (SKAttention_conv if image_size > 4 else SKAttention_fc)(out_planes, m)
 
     def forward(self, x, w):
-        feas = [getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
+        if SK_BRANCHES[0]:
+            feas = [None] * self.M
+            with ops.Branches(x.device, self.M) as br:      # the k3 / k5 branches are independent
+                for i in range(self.M):
+                    with br[i]:
+                        feas[i] = getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight)
+        else:
+            feas = [getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
         return _mix(feas, self.sk_attention(feas))
 
 
@@ -327,6 +341,11 @@ class ResnetInit(nn.Module):
 
     def forward(self, x, w):
         x_res, x_tr = x
+        if not RESNET_BRANCHES[0]:
+            r_r, r_t = self.residual(x_res, w), self.residual_across(x_res, w)
+            t_t, t_r = self.transient(x_tr, w), self.transient_across(x_tr, w)
+            return (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
+                    ops.add_prelu(r_t, t_t, self.activation_transient.weight))
         # the four StyleBlocks are independent: on a GPU each runs on its own HIP stream (their
         # hundreds of small, launch-bound kernels overlap; a captured graph keeps the branches),
         # issued in the reference's order so the noise draws keep theirs
