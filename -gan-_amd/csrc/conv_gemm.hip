@@ -175,6 +175,7 @@ struct WgradArgs {
   int om, oj, ot;
   float alpha;
   int kt_per_split, splits, accumulate;
+  int T;               // taps (tap-packed launches: the GEMM's N is (tap, channel) pairs)
   float* slab;         // split-K: per-split partial weights [split][numel(out)] (null: single split)
   int out_numel;
   int bf16;
@@ -827,7 +828,10 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
 // ------------------------------------------------------------------------------------------
 // wgrad: K = output pixels n, M = output channels of the conv, N = gathered channels at tap t
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED, bool BF16>
+// TP (tap-packed): the N dimension runs over (tap, channel) pairs, n = t*J + j, so narrow gathered
+// sides (J = 3, 48, 96 against 64/128-wide tiles) fill their tiles across taps instead of padding
+// every tap's tile; each B row then has its own tap.
+template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED, bool BF16, bool TP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD_WGRAD_WPE)))
 void wgrad_gemm_kernel(WgradArgs p) {
   using C = TileCfg<BM, BN, WGM, WGN>;
@@ -848,7 +852,7 @@ void wgrad_gemm_kernel(WgradArgs p) {
   // pixel ranges of gy and x).  A tap-fastest order with an XCD-contiguous remap, meant to share
   // the taps' overlapping source rows through one XCD's L2, measured 5-15 % slower.
   const int j0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int t = blockIdx.z / p.splits;
+  const int t = TP ? 0 : blockIdx.z / p.splits;
   const int split = blockIdx.z - t * p.splits;
   const int kt_total = (p.K + BKW - 1) / BKW;
   const int kt0 = split * p.kt_per_split;
@@ -860,6 +864,14 @@ void wgrad_gemm_kernel(WgradArgs p) {
   const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
   const int tk = tid % BKW;   // B: pixel fixed per thread
   const int tr = tid / BKW;   // B: channel base
+  // TP: (tap, channel, kh, kw) of this thread's first B row, stepped by RSTEP rows per e
+  int tp_t = 0, tp_j = 0, tp_kh = 0, tp_kw = 0;
+  if (TP) {
+    tp_t = (j0 + tr) / p.J;
+    tp_j = j0 + tr - tp_t * p.J;
+    tp_kh = tp_t / g.KW;
+    tp_kw = tp_t - tp_kh * g.KW;
+  }
 
   const rsrc_t ra_r = make_rsrc(p.a, p.a_bytes);
   const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
@@ -912,7 +924,8 @@ void wgrad_gemm_kernel(WgradArgs p) {
     // (pb, poh, pow)), channels j0 + tr + e*RSTEP
     const int n = kt * BKW + tk;
     const int b = pb;
-    const int sp = n < p.K ? tap_offset<MODE>(g, poh, pow_, kh, kw) : -1;
+    const int poh_cur = poh, pow_cur = pow_;
+    const int sp = (!TP && n < p.K) ? tap_offset<MODE>(g, poh, pow_, kh, kw) : -1;
     pow_ += d_ow;
     if (pow_ >= g.OW) {
       pow_ -= g.OW;
@@ -925,6 +938,25 @@ void wgrad_gemm_kernel(WgradArgs p) {
     }
     pb += d_b;
     // channels past the source's end fall outside the buffer: the hardware returns 0
+    if constexpr (TP) {
+      int te = tp_t, je = tp_j, khe = tp_kh, kwe = tp_kw;
+#pragma unroll
+      for (int e = 0; e < EB; ++e) {
+        const int spe = (n < p.K && te < p.T) ? tap_offset<MODE>(g, poh_cur, pow_cur, khe, kwe) : -1;
+        rb[e] = bload(rx, spe >= 0 ? (int)(4u * (unsigned)(b * g.H * g.W + spe) + (unsigned)je * cs4) : kOOB);
+        if (SCALED) rsb[e] = bload(rsb_r, spe >= 0 ? 4 * (je * g.B + b) : kOOB);
+        je += RSTEP;
+        while (je >= p.J) {
+          je -= p.J;
+          ++te;
+          if (++kwe == g.KW) {
+            kwe = 0;
+            ++khe;
+          }
+        }
+      }
+      return;
+    }
     const unsigned base = sp >= 0 ? 4u * (unsigned)(b * g.H * g.W + sp) + (unsigned)(j0 + tr) * cs4 : (unsigned)kOOB;
     const unsigned sbase = sp >= 0 ? 4u * (unsigned)((j0 + tr) * g.B + b) : (unsigned)kOOB;
 #pragma unroll
@@ -985,15 +1017,22 @@ void wgrad_gemm_kernel(WgradArgs p) {
 
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
-    const int jj = j0 + (wn * C::TN + j) * 32 + (lane & 31);
-    if (jj >= p.J) continue;
+    int jj = j0 + (wn * C::TN + j) * 32 + (lane & 31);
+    int tt = t;
+    if (TP) {
+      if (jj >= p.T * p.J) continue;
+      tt = jj / p.J;
+      jj -= tt * p.J;
+    } else if (jj >= p.J) {
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
-        const int o = m * p.om + jj * p.oj + t * p.ot;
+        const int o = m * p.om + jj * p.oj + tt * p.ot;
         const float v = p.alpha * acc[i][j][r];
         if (p.slab)
           p.slab[(long)split * p.out_numel + o] = v;
@@ -1082,6 +1121,10 @@ int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
+int wgrad_tp_enabled() {   // GANAMD_WGRAD_TP=0: one tile column set per tap (A/B)
+  static const int v = env_int("GANAMD_WGRAD_TP", 1);
+  return v;
+}
 int linear_enabled() {   // GANAMD_LINEAR=0: linears through the tiled conv GEMM (A/B)
   static const int v = env_int("GANAMD_LINEAR", 1);
   return v;
@@ -1108,6 +1151,7 @@ int wgrad_lds_pad() {
 // and the launch agree.
 struct Plan {
   int bm, bn, splits, kt_per_split;
+  int tp = 0;          // wgrad: taps packed into N (see wgrad_gemm_kernel TP)
 };
 
 // Row tile: the least padded rows per unit of tile efficiency (measured: 96-row tiles ~0.95 and
@@ -1333,7 +1377,7 @@ template <int BM, int BN, int WGM, int WGN, bool SCALED>
 int wgrad_occ() {
   static const int v = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wgrad_gemm_kernel<BM, BN, WGM, WGN, kReplicate, SCALED, false>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wgrad_gemm_kernel<BM, BN, WGM, WGN, kReplicate, SCALED, false, false>,
                                                      kThreads, wgrad_lds_pad()) != hipSuccess || n <= 0)
       n = 2;
     return n;
@@ -1358,9 +1402,17 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
     bm = 64;
     bn = 64;
   }
-  const int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
+  int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
+  // tap-packed N = (tap, channel) for very narrow gathered sides (the critic's 3-channel input
+  // conv: 27 of 576 tile columns used per tap otherwise; 1.85x measured).  For J = 48..192 the
+  // per-row tap offsets cost more than the padding they remove (3-13 % slower, tools/ab_shapes.py)
+  const int tiles_tp = ((T * J + bn - 1) / bn) * ((M + bm - 1) / bm);
+  const bool tp = T > 1 && J < 32 && tiles_tp <= 0.5 * tiles && wgrad_tp_enabled();
+  if (tp) tiles = tiles_tp;
   const int occ = scaled ? wgrad_occ_tile<true>(bm, bn) : wgrad_occ_tile<false>(bm, bn);
-  return split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, 2.0 * bm * bn * BKW, (long)M * J * T, occ, 256, 4);
+  Plan pl = split_plan(bm, bn, tiles, (K + BKW - 1) / BKW, 2.0 * bm * bn * BKW, (long)M * J * T, occ, 256, 4);
+  pl.tp = tp;
+  return pl;
 }
 
 // Folds the S partial slabs of the tail columns [n0, n0 + cols) and applies the epilogue.
@@ -1575,12 +1627,17 @@ hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab,
 
 template <int BM, int BN, int WGM, int WGN, int MODE, bool SCALED, bool BF16>
 hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStream_t st) {
-  const int gx = (p.J + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
+  const int gy = (p.M + BM - 1) / BM;
   p.kt_per_split = pl.kt_per_split;
   p.splits = pl.splits;
   p.slab = pl.splits > 1 ? slab : nullptr;
-  hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED, BF16>), dim3(gx, gy, T * pl.splits), dim3(kThreads),
-                     wgrad_lds_pad(), st, p);
+  p.T = T;
+  if (pl.tp)
+    hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED, BF16, true>),
+                       dim3((T * p.J + BN - 1) / BN, gy, pl.splits), dim3(kThreads), wgrad_lds_pad(), st, p);
+  else
+    hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED, BF16, false>),
+                       dim3((p.J + BN - 1) / BN, gy, T * pl.splits), dim3(kThreads), wgrad_lds_pad(), st, p);
   if (pl.splits > 1)
     hipLaunchKernelGGL(wgrad_split_reduce_kernel, dim3(grid1d(p.out_numel)), dim3(256), 0, st, slab, pl.splits,
                        p.out_numel, p.out, p.accumulate);

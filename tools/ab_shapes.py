@@ -11,6 +11,15 @@ import os
 import subprocess
 import sys
 
+import os as _os
+SHAPES_WGRAD = [
+    ("wgrad", 64, 96, 64, 96, 5, 1, 2, True, 10),
+    ("wgrad", 64, 48, 64, 48, 5, 1, 2, True, 20),
+    ("wgrad", 64, 48, 64, 48, 3, 1, 1, True, 30),
+    ("wgrad", 64, 192, 16, 192, 5, 1, 2, True, 10),
+    ("wgrad", 128, 3, 64, 64, 3, 1, 1, False, 5),
+    ("wgrad", 64, 96, 32, 96, 3, 1, 1, True, 30),
+]
 SHAPES = [  # (op, B, cin, H, cout, k, stride, pad, scaled, weight = launches per iteration)
     ("fwd", 64, 96, 64, 96, 5, 1, 2, True, 60),
     ("fwd", 64, 48, 64, 48, 5, 1, 2, True, 120),
@@ -34,7 +43,7 @@ def child():
     from gan_amd import ops
     dev = torch.device("cuda")
     tot_t = tot_f = 0.0
-    for op, B, cin, H, cout, k, s, p, scaled, n in SHAPES:
+    for op, B, cin, H, cout, k, s, p, scaled, n in (SHAPES_WGRAD if _os.environ.get("AB_SET") == "wgrad" else SHAPES):
         g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
         x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
         y = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
