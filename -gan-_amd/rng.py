@@ -9,26 +9,42 @@ from __future__ import annotations
 
 import torch
 
+from . import _lib
+
 
 class DeviceRNG:
+    """Philox4x32-10 draws on the device (csrc/rng.hip, ganamd_philox_*).
+
+    The stream offset is a device-resident counter that every draw advances on the stream, so
+    draws issued inside a captured HIP graph are fresh on every replay.  The seed defaults to
+    torch's initial seed, so ``torch.manual_seed`` makes a run repeatable as in the reference.
+    """
+
     def __init__(self, device, seed: int | None = None):
         self.device = torch.device(device)
-        if seed is not None:
-            torch.cuda.manual_seed(seed)
+        self.seed = int(torch.initial_seed() if seed is None else seed) & 0xFFFFFFFFFFFFFFFF
+        self.offset = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    def _draw(self, fn, shape):
+        out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        n = out.numel()
+        if n:
+            _lib.check(fn(out.data_ptr(), n, self.seed, self.offset.data_ptr(), _lib.stream()), fn.__name__)
+        return out
 
     def randn(self, shape):
-        return torch.randn(shape, device=self.device)
+        return self._draw(_lib.LIB.ganamd_philox_normal, shape)
 
     def rand(self, shape):
-        return torch.rand(shape, device=self.device)
+        return self._draw(_lib.LIB.ganamd_philox_uniform, shape)
 
     def noise(self, shape_nchw):
         B, C, H, W = shape_nchw
-        return torch.randn((C, B, H, W), device=self.device)
+        return self.randn((C, B, H, W))
 
     def noise_bulk(self, numel):
         """All of one generator forward's noise in one draw (generator_13_5._NoiseHub)."""
-        return torch.randn(numel, device=self.device)
+        return self.randn((numel,))
 
 
 class ReplayRNG:

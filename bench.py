@@ -288,10 +288,10 @@ def build(args, dev, rank):
         D = gan_amd.Discriminator().to(dev)
     torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
     if args.config == "lazy":
-        tr = gan_amd.wganlazygpR2.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev),
+        tr = gan_amd.wganlazygpR2.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev, 4321 + rank),
                                         precision=args.precision)
     else:
-        tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev))
+        tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev, 4321 + rank))
     B = args.batch
 
     def real():

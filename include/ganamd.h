@@ -330,6 +330,20 @@ int ganamd_mbstd_tangent(const float* x, const float* xd, long ldx, int C, int B
 int ganamd_mbstd_adjoint(const float* x, const float* xd, long ldx, const float* gy, const float* ay, long ldy, int C,
                          int B, int HW, int S, int G, float* ax, void* workspace, hipStream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Device random numbers (Philox4x32-10) for z, eps and the StyleConv noise.
+ * Replaces torch.randn / torch.rand on the path (train/wgangp.py:22,35,58;
+ * generator_13_5.py:265; train/gan.py:21,32 label noise).  Element 4g+i of a draw is word i of
+ * Philox4x32-10(counter {g lo, g hi, off lo, off hi}, key {seed lo, seed hi}) where off = *offset
+ * read on the device; the call then advances *offset by one on the stream (graph-replay safe).
+ *   uniform: (word >> 8) * 2^-24 in [0, 1)
+ *   normal:  Box-Muller on (w0, w1) and (w2, w3): u1 = ((w >> 8) + 1) * 2^-24, u2 = (w >> 8) * 2^-24,
+ *            z = sqrt(-2 ln u1) * (cos, sin)(2 pi u2)
+ * offset: device pointer to one uint64.  n > 0.
+ * ------------------------------------------------------------------------------------- */
+int ganamd_philox_uniform(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream);
+int ganamd_philox_normal(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream);
+
 /* Library identification (for load checks). */
 const char* ganamd_version(void);
 
