@@ -1416,34 +1416,79 @@ Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
 }
 
 // Folds the S partial slabs of the tail columns [n0, n0 + cols) and applies the epilogue.
-__global__ void conv_split_reduce_kernel(const float* __restrict__ slab, int S, int M, int cols, int n0, long ldy,
-                                         int ohw, int B, const float* __restrict__ oscale,
-                                         const float* __restrict__ bias, const float* __restrict__ noise,
-                                         const float* __restrict__ noise_scale, const float* __restrict__ act,
-                                         float* __restrict__ y, OutMap om) {
-  const long total = (long)M * cols;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += slab[s * total + i];
-    const int m = (int)(i / cols);
-    const int n = n0 + (int)(i - (long)m * cols);
-    const long o = (long)m * ldy + out_col(om, n);
-    if (oscale) v *= oscale[m * B + n / ohw];
-    if (bias) v += bias[m];
-    if (noise) v += noise_scale[m] * noise[o];
-    if (act) v = v > 0.f ? v : act[m] * v;
-    y[o] = v;
+// Memory-bound: (S + 1) x M x cols floats.  32-bit element indices (M * cols < 2^31 is checked by
+// the launcher) and, when every row segment is a whole number of 16-byte vectors landing on
+// 16-byte aligned output addresses (VEC), four columns per thread with one row division.
+template <bool VEC>
+__global__ __launch_bounds__(256) void conv_split_reduce_kernel(
+    const float* __restrict__ slab, int S, int M, int cols, int n0, long ldy, int ohw, int B,
+    const float* __restrict__ oscale, const float* __restrict__ bias, const float* __restrict__ noise,
+    const float* __restrict__ noise_scale, const float* __restrict__ act, float* __restrict__ y, OutMap om) {
+  constexpr int V = VEC ? 4 : 1;
+  const unsigned total = (unsigned)M * (unsigned)cols, cv = (unsigned)cols / V, units = total / V;
+  for (unsigned u = blockIdx.x * 256u + threadIdx.x; u < units; u += gridDim.x * 256u) {
+    const unsigned m = u / cv, c = (u - m * cv) * V;
+    const unsigned e = m * (unsigned)cols + c;
+    float v[V];
+    if constexpr (VEC) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(slab + e);
+      for (int s = 1; s < S; ++s) a += *reinterpret_cast<const f32x4*>(slab + (long)s * total + e);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    } else {
+      float a = slab[e];
+      for (int s = 1; s < S; ++s) a += slab[(long)s * total + e];
+      v[0] = a;
+    }
+    const int n = n0 + (int)c;
+    const long o = (long)m * ldy + out_col(om, n);   // VEC: om is the identity, o .. o + 3 contiguous
+    const float bm = bias ? bias[m] : 0.f, ns = noise ? noise_scale[m] : 0.f, am = act ? act[m] : 1.f;
+    float nz[V];
+    if (noise) {
+      if constexpr (VEC) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(noise + o);
+        nz[0] = t[0]; nz[1] = t[1]; nz[2] = t[2]; nz[3] = t[3];
+      } else {
+        nz[0] = noise[o];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      float r = v[q];
+      if (oscale) r *= oscale[m * B + (unsigned)(n + q) / (unsigned)ohw];
+      r += bm;
+      if (noise) r += ns * nz[q];
+      if (act) r = r > 0.f ? r : am * r;
+      v[q] = r;
+    }
+    if constexpr (VEC) {
+      *reinterpret_cast<f32x4*>(y + o) = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+      y[o] = v[0];
+    }
   }
 }
 
-__global__ void wgrad_split_reduce_kernel(const float* __restrict__ slab, int S, int total, float* __restrict__ out,
-                                          int accumulate) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += slab[(long)s * total + i];
-    out[i] = accumulate ? out[i] + v : v;
+template <bool VEC>
+__global__ __launch_bounds__(256) void wgrad_split_reduce_kernel(const float* __restrict__ slab, int S, int total,
+                                                                 float* __restrict__ out, int accumulate) {
+  constexpr int V = VEC ? 4 : 1;
+  const unsigned units = (unsigned)total / V;
+  for (unsigned u = blockIdx.x * 256u + threadIdx.x; u < units; u += gridDim.x * 256u) {
+    const unsigned e = u * V;
+    if constexpr (VEC) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(slab + e);
+      for (int s = 1; s < S; ++s) a += *reinterpret_cast<const f32x4*>(slab + (long)s * total + e);
+      if (accumulate) a += *reinterpret_cast<const f32x4*>(out + e);
+      *reinterpret_cast<f32x4*>(out + e) = a;
+    } else {
+      float a = slab[e];
+      for (int s = 1; s < S; ++s) a += slab[(long)s * total + e];
+      out[e] = accumulate ? out[e] + a : a;
+    }
   }
 }
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int grid1d(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
 
@@ -1460,10 +1505,20 @@ hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t 
   const long blocks = (long)p.full_blocks + (long)(pl.gx - pl.nfull_t) * pl.gy * pl.S;
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WGM, WGN, MODE, BSCALE, BF16>), dim3((unsigned)blocks), dim3(kThreads),
                      conv_lds_pad(), st, p);
-  if (pl.slab_elems)
-    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(grid1d((long)p.M * p.tail_cols)), dim3(256), 0, st, slab, pl.S,
-                       p.M, p.tail_cols, p.tail_n0, p.ldy, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
-                       p.y, p.om);
+  if (pl.slab_elems) {
+    const long total = (long)p.M * p.tail_cols;
+    if (total >= (1L << 31)) return hipErrorInvalidValue;
+    const bool vec = p.om.s == 0 && p.tail_cols % 4 == 0 && p.tail_n0 % 4 == 0 && p.ldy % 4 == 0 && aligned16(slab) &&
+                     aligned16(p.y) && (!p.noise || aligned16(p.noise));
+    if (vec)
+      hipLaunchKernelGGL(conv_split_reduce_kernel<true>, dim3(grid1d(total / 4)), dim3(256), 0, st, slab, pl.S, p.M,
+                         p.tail_cols, p.tail_n0, p.ldy, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
+                         p.y, p.om);
+    else
+      hipLaunchKernelGGL(conv_split_reduce_kernel<false>, dim3(grid1d(total)), dim3(256), 0, st, slab, pl.S, p.M,
+                         p.tail_cols, p.tail_n0, p.ldy, p.ohw, p.g.B, p.oscale, p.bias, p.noise, p.noise_scale, p.act,
+                         p.y, p.om);
+  }
   return hipGetLastError();
 }
 
@@ -1638,9 +1693,14 @@ hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStre
   else
     hipLaunchKernelGGL((wgrad_gemm_kernel<BM, BN, WGM, WGN, MODE, SCALED, BF16, false>),
                        dim3((p.J + BN - 1) / BN, gy, T * pl.splits), dim3(kThreads), wgrad_lds_pad(), st, p);
-  if (pl.splits > 1)
-    hipLaunchKernelGGL(wgrad_split_reduce_kernel, dim3(grid1d(p.out_numel)), dim3(256), 0, st, slab, pl.splits,
-                       p.out_numel, p.out, p.accumulate);
+  if (pl.splits > 1) {
+    if (p.out_numel % 4 == 0 && aligned16(slab) && aligned16(p.out))
+      hipLaunchKernelGGL(wgrad_split_reduce_kernel<true>, dim3(grid1d(p.out_numel / 4)), dim3(256), 0, st, slab,
+                         pl.splits, p.out_numel, p.out, p.accumulate);
+    else
+      hipLaunchKernelGGL(wgrad_split_reduce_kernel<false>, dim3(grid1d(p.out_numel)), dim3(256), 0, st, slab,
+                         pl.splits, p.out_numel, p.out, p.accumulate);
+  }
   return hipGetLastError();
 }
 
