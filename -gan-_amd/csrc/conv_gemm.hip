@@ -183,11 +183,22 @@ struct WgradArgs {
 
 template <int BM, int BN, int WGM, int WGN>
 struct TileCfg {
-  static constexpr int TM = BM / (32 * WGM);
-  static constexpr int TN = BN / (32 * WGN);
+  // MFMA block edge: 32 (v_mfma_f32_32x32x2_f32) unless a wave's sub-tile is not a multiple of
+  // 32 (48-row conv tiles, 96-wide wgrad tiles: v_mfma_f32_16x16x4_f32, same FLOP rate per CU,
+  // 16-granular tiles)
+  static constexpr int MB = ((BM / WGM) % 32 == 0 && (BN / WGN) % 32 == 0) ? 32 : 16;
+  static constexpr int TM = BM / (MB * WGM);
+  static constexpr int TN = BN / (MB * WGN);
+  static constexpr int NR = MB == 32 ? 16 : 4;   // accumulator registers per block and lane
+  using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
   static_assert(WGM * WGN == 4, "4 waves per block");
-  static_assert(TM * 32 * WGM == BM && TN * 32 * WGN == BN, "tile must split into 32x32 MFMAs");
+  static_assert(TM * MB * WGM == BM && TN * MB * WGN == BN, "tile must split into MFMA blocks");
 };
+// C/D map of the block MFMAs: lane's register r holds row mfma_row<MB>(lane, r), column lane % MB
+template <int MB>
+__device__ __forceinline__ int mfma_row(int lane, int r) {
+  return MB == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : 4 * (lane >> 4) + r;
+}
 
 // Read this lane's 8 k-values of one 32-row fragment: rows r of the [row][k] tile, k = 8h..8h+7.
 template <int LD>
@@ -220,7 +231,33 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 // B[8h + j][r], j = 0..7) and its C/D map that of 32x32x2 f32, so nothing else changes.
 template <class C, int LD = LDK, bool BF16 = false>
 __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
-                                          f32x16 (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0) {
+                                          typename C::acc_t (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0) {
+  if constexpr (C::MB == 16) {
+    // 16x16x4: lane (r, q) supplies A[r][k0 + 4q + s] and B[k0 + 4q + s][r] in step s = 0..3
+    static_assert(!BF16, "16-row tiles are fp32 only");
+    const int r = lane & 15, q = lane >> 4;
+    float a[C::TM][4], b[C::TN][4];
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i) {
+      const float* src = As + ((wm * C::TM + i) * 16 + r) * LD + k0 + 4 * q;
+      const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
+      a[i][0] = t0[0]; a[i][1] = t0[1]; a[i][2] = t1[0]; a[i][3] = t1[1];
+    }
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) {
+      const float* src = Bs + ((wn * C::TN + j) * 16 + r) * LD + k0 + 4 * q;
+      const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
+      b[j][0] = t0[0]; b[j][1] = t0[1]; b[j][2] = t1[0]; b[j][3] = t1[1];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    return;
+  } else {
   const int r = lane & 31, h = lane >> 5;
   float a[C::TM][8], b[C::TN][8];
 #pragma unroll
@@ -257,16 +294,17 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
 #ifdef GANAMD_SETPRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
+  }
 }
 
 template <class C>
-__device__ __forceinline__ void zero_acc(f32x16 (&acc)[C::TM][C::TN]) {
+__device__ __forceinline__ void zero_acc(typename C::acc_t (&acc)[C::TM][C::TN]) {
 #pragma unroll
   for (int i = 0; i < C::TM; ++i)
 #pragma unroll
     for (int j = 0; j < C::TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < C::NR; ++r) acc[i][j][r] = 0.f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -701,7 +739,7 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
           BSCALE ? f32x2{rb[e] * rs[e], rb[e + 1] * rs[e + 1]} : f32x2{rb[e], rb[e + 1]};
   };
 
-  f32x16 acc[C::TM][C::TN];
+  typename C::acc_t acc[C::TM][C::TN];
   zero_acc<C>(acc);
 
   Stage s0;
@@ -745,22 +783,22 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
   }
 #endif
 
-  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-  // Split-K blocks store raw partial tiles to their slab; the reduce kernel applies the rest.
+  // epilogue: C/D map of the block MFMA (mfma_row).  Split-K blocks store raw partial tiles to
+  // their slab; the reduce kernel applies the rest.
   const bool finish = split < 0 || p.S == 1;
   float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
   const long ldo = finish ? p.ldy : p.tail_cols;
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
-    const int n = n0 + (wn * C::TN + j) * 32 + (lane & 31);
+    const int n = n0 + (wn * C::TN + j) * C::MB + (lane & (C::MB - 1));
     if (n >= p.N) continue;
     const int b = (finish && p.oscale) ? n / p.ohw : 0;
     const long col = (MODE == kPhase && finish) ? out_col(p.om, n) : n;
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      for (int r = 0; r < C::NR; ++r) {
+        const int m = m0 + (wm * C::TM + i) * C::MB + mfma_row<C::MB>(lane, r);
         if (m >= p.M) continue;
         float v = p.alpha * acc[i][j][r];
         if (finish) {
@@ -883,6 +921,7 @@ void wgrad_gemm_kernel(WgradArgs p) {
 
   f32x4 ra[EA], rsa[EA];
   float rb[EB], rsb[EB];
+  int sb_b = -1;   // sample whose B-side scales rsb holds (SCALED, not TP)
   // pixel of this thread's B column for the next K-step, advanced by BKW pixels per step
   const int d_b = BKW / p.ohw, d_rem = BKW - d_b * p.ohw, d_oh = d_rem / g.OW, d_ow = d_rem - d_oh * g.OW;
   int pb, poh, pow_;
@@ -958,11 +997,16 @@ void wgrad_gemm_kernel(WgradArgs p) {
       return;
     }
     const unsigned base = sp >= 0 ? 4u * (unsigned)(b * g.H * g.W + sp) + (unsigned)(j0 + tr) * cs4 : (unsigned)kOOB;
-    const unsigned sbase = sp >= 0 ? 4u * (unsigned)((j0 + tr) * g.B + b) : (unsigned)kOOB;
 #pragma unroll
-    for (int e = 0; e < EB; ++e) {
-      rb[e] = bload(rx, (int)(base + (unsigned)(e * RSTEP) * cs4));
-      if (SCALED) rsb[e] = bload(rsb_r, (int)(sbase + 4u * (unsigned)(e * RSTEP * g.B)));
+    for (int e = 0; e < EB; ++e) rb[e] = bload(rx, (int)(base + (unsigned)(e * RSTEP) * cs4));
+    // the B-side scales s[j][b] change only when this thread's pixel enters the next sample
+    // (every ohw / BKW K-steps): reload them then, not per step.  Where the gather is out of
+    // range rb is 0, so a stale or out-of-range scale there multiplies 0.
+    if (SCALED && b != sb_b) {
+      sb_b = b;
+      const unsigned sbase = 4u * (unsigned)((j0 + tr) * g.B + b);
+#pragma unroll
+      for (int e = 0; e < EB; ++e) rsb[e] = bload(rsb_r, (int)(sbase + 4u * (unsigned)(e * RSTEP * g.B)));
     }
   };
   auto sstore = [&](int buf) {
@@ -994,7 +1038,7 @@ void wgrad_gemm_kernel(WgradArgs p) {
     }
   };
 
-  f32x16 acc[C::TM][C::TN];
+  typename C::acc_t acc[C::TM][C::TN];
   zero_acc<C>(acc);
 
   gload(kt0);
@@ -1017,7 +1061,7 @@ void wgrad_gemm_kernel(WgradArgs p) {
 
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
-    int jj = j0 + (wn * C::TN + j) * 32 + (lane & 31);
+    int jj = j0 + (wn * C::TN + j) * C::MB + (lane & (C::MB - 1));
     int tt = t;
     if (TP) {
       if (jj >= p.T * p.J) continue;
@@ -1029,8 +1073,8 @@ void wgrad_gemm_kernel(WgradArgs p) {
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (wm * C::TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      for (int r = 0; r < C::NR; ++r) {
+        const int m = m0 + (wm * C::TM + i) * C::MB + mfma_row<C::MB>(lane, r);
         if (m >= p.M) continue;
         const int o = m * p.om + jj * p.oj + tt * p.ot;
         const float v = p.alpha * acc[i][j][r];
@@ -1157,8 +1201,13 @@ struct Plan {
 // Row tile: the least padded rows per unit of tile efficiency (measured: 96-row tiles ~0.95 and
 // 64-row ~0.9 of the 128-row rate) -- e.g. M = 192 takes two 96-row tiles, not two 128-row ones
 // (256 rows, 25 % empty); a smaller tile has to beat the 128-row one by 5 %.
+int tile48() {   // GANAMD_TILE48=0: M = 33..48 on the 64-row tile (A/B)
+  static const int v = env_int("GANAMD_TILE48", 1);
+  return v;
+}
 int conv_bm(int M) {
   if (M <= 32) return 32;
+  if (M <= 48 && tile48()) return 48;   // 16x16x4 MFMA blocks: 48 rows without 64-row padding
   if (M <= 64) return 64;
   if (M <= 96) return 96;
   const double c128 = (M + 127) / 128 * 128.0, c96 = (M + 95) / 96 * 96.0 / 0.95, c64 = (M + 63) / 64 * 64.0 / 0.9;
@@ -1170,6 +1219,10 @@ int wide_tiles() {   // GANAMD_WIDE=1: 128 x 256 tiles (2 waves per SIMD) for M 
   return v;
 }
 int conv_bn(int bm, int) { return bm == 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
+int tile96() {   // GANAMD_TILE96=0: wgrad keeps 128-wide tiles on J = 96, 192 (A/B)
+  static const int v = env_int("GANAMD_TILE96", 1);
+  return v;
+}
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
 
 // Split-K: pure functions of the geometry (the workspace query and the launch agree).
@@ -1253,6 +1306,9 @@ template <int MODE, bool BSCALE, bool BF16>
 int conv_occ_tile(int bm, int bn) {
   switch (bm) {
     case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE, BF16>();
+    case 48:
+      if constexpr (!BF16) return conv_occ<48, 128, 1, 4, MODE, BSCALE, BF16>();
+      return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
     case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
     case 96: return conv_occ<96, 128, 1, 4, MODE, BSCALE, BF16>();
     default: return bn == 256 ? conv_occ<128, 256, 2, 2, MODE, BSCALE, BF16>() : conv_occ<128, 128, 2, 2, MODE, BSCALE, BF16>();
@@ -1314,6 +1370,9 @@ constexpr double kSustainedTflopsBf16 = 300.0;   // the bf16-LDS body (conv_body
 ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {
   ConvPlan pl{};
   conv_tile(M, &pl.bm, &pl.bn);
+  // the bf16 body has 32x32 blocks only: its 48-row GEMMs run on the 64-row tile over the same
+  // 48-row packed operand (rows past it read as 0 through the buffer bound, are not stored)
+  if (bf16 && pl.bm == 48) pl.bm = 64;
   pl.gx = (N + pl.bn - 1) / pl.bn;
   pl.gy = (M + pl.bm - 1) / pl.bm;
   // bf16 kernels take K-steps of BKB = two fp32 steps (conv_body_bf16)
@@ -1388,6 +1447,7 @@ int wgrad_occ() {
 template <bool SCALED>
 int wgrad_occ_tile(int bm, int bn) {
   if (bn == 64) return wgrad_occ<64, 64, 2, 2, SCALED>();
+  if (bn == 96) return bm == 96 ? wgrad_occ<96, 96, 2, 2, SCALED>() : wgrad_occ<64, 96, 2, 2, SCALED>();
   switch (bm) {
     case 32: return wgrad_occ<32, 128, 1, 4, SCALED>();
     case 64: return wgrad_occ<64, 128, 2, 2, SCALED>();
@@ -1396,11 +1456,13 @@ int wgrad_occ_tile(int bm, int bn) {
   }
 }
 
-Plan wgrad_plan(int M, int J, int K, int T, bool scaled) {
+Plan wgrad_plan(int M, int J, int K, int T, bool scaled, bool bf16) {
   int bm = wgrad_bm(M, scaled), bn = 128;
   if (J <= 64 && bm >= 64) {  // narrow gathered side: a 64x64 tile wastes nothing on J = 48..64
     bm = 64;
     bn = 64;
+  } else if ((bm == 64 || bm == 96) && !bf16 && tile96() && (J + 95) / 96 * 96 / 0.97 < 0.95 * ((J + 127) / 128 * 128)) {
+    bn = 96;   // J = 96, 192, ...: 96-wide tiles (16x16x4 blocks) instead of 25 % empty 128-wide ones
   }
   int tiles = ((J + bn - 1) / bn) * ((M + bm - 1) / bm) * T;
   // tap-packed N = (tap, channel) for very narrow gathered sides (the critic's 3-channel input
@@ -1526,6 +1588,9 @@ template <int MODE, bool BSCALE, bool BF16>
 hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab, hipStream_t st) {
   switch (pl.bm) {
     case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
+    case 48:
+      if constexpr (!BF16) return launch_conv<48, 128, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
+      return hipErrorInvalidValue;   // conv_plan moves bf16 to the 64-row tile
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
     case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
     default:
@@ -1667,7 +1732,8 @@ hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
   const ConvPlan pl = conv_plan(p.M, p.N, p.Ck, p.T, p.g.mode, p.g.scale != nullptr, p.bf16 != 0);
   if ((pl.slab_elems && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
-  const int mpad = (p.M + pl.bm - 1) / pl.bm * pl.bm;
+  const int bmp = conv_bm(p.M);   // packing granularity (pl.bm may be wider: bf16 48 -> 64)
+  const int mpad = (p.M + bmp - 1) / bmp * bmp;
   p.Ckp = (p.Ck + BK - 1) / BK * BK;
   if (p.ldy == 0) p.ldy = p.N;   // output rows are the GEMM rows unless a phase remap says otherwise
   if (!prepacked) {
@@ -1707,6 +1773,12 @@ hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStre
 template <int MODE, bool SCALED, bool BF16>
 hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, const Plan& pl, float* slab, hipStream_t st) {
   if (pl.bn == 64) return launch_wgrad<64, 64, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
+  if (pl.bn == 96) {   // 16x16x4 blocks: fp32 only (wgrad_plan gives bf16 128-wide tiles)
+    if constexpr (!BF16)
+      return pl.bm == 96 ? launch_wgrad<96, 96, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st)
+                         : launch_wgrad<64, 96, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
+    return hipErrorInvalidValue;
+  }
   switch (pl.bm) {
     case 32: return launch_wgrad<32, 128, 1, 4, MODE, SCALED, BF16>(p, T, pl, slab, st);
     case 64: return launch_wgrad<64, 128, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
@@ -1718,7 +1790,7 @@ hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, const Plan& pl, float*
 hipError_t dispatch_wgrad(const WgradArgs& p, int T, float* slab, hipStream_t st) {
   const bool s = p.ascale != nullptr || p.g.scale != nullptr;
   if (s && !(p.ascale && p.g.scale)) return hipErrorInvalidValue;  // both scales or none
-  const Plan pl = wgrad_plan(p.M, p.J, p.K, T, s);
+  const Plan pl = wgrad_plan(p.M, p.J, p.K, T, s, p.bf16 != 0);
   if (pl.splits > 1 && !slab) return hipErrorInvalidValue;
   if (p.bf16) {
     if (p.g.mode == kReplicate)
@@ -1935,7 +2007,8 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
     T = d->KH * d->KW;
     const int Mw = d->transposed ? d->Cin : d->Cout, Jw = d->transposed ? d->Cout : d->Cin;
     // the modulated (scaled) variant plans the same or more splits; size for the larger
-    const Plan a = wgrad_plan(Mw, Jw, Kpix, T, false), b = wgrad_plan(Mw, Jw, Kpix, T, true);
+    const bool bf = d->math == GANAMD_MATH_BF16;
+    const Plan a = wgrad_plan(Mw, Jw, Kpix, T, false, bf), b = wgrad_plan(Mw, Jw, Kpix, T, true, bf);
     const int S = std::max(a.splits, b.splits);
     *bytes = S > 1 ? sizeof(float) * (size_t)S * d->Cin * d->Cout * T : 0;
   } else {

@@ -41,6 +41,9 @@ CONV_CASES = [
     # B, Cin, H, Cout, k, stride, pad, mode
     (4, 5, 8, 7, 3, 1, 1, 1),
     (2, 48, 16, 48, 5, 1, 2, 1),
+    # 33..48 output rows take the 48-row tile (16x16x4 MFMA blocks); ragged rows, split tails
+    (4, 40, 16, 45, 3, 1, 1, 1),
+    (8, 48, 32, 48, 3, 1, 1, 0),
     (4, 16, 8, 33, 3, 2, 1, 1),
     (3, 20, 5, 20, 3, 1, 0, 0),
     (4, 17, 6, 9, 1, 1, 0, 0),
@@ -141,7 +144,7 @@ def test_linear(ops, B, cin, cout):
     assert rel(xa.grad.t(), gx) < 1e-4 and rel(wa.grad, gw) < 1e-4 and rel(ba.grad, gb) < 1e-4
 
 
-@pytest.mark.parametrize("B,cin,cout,H,k", [(4, 48, 54, 16, 3), (4, 96, 96, 8, 5), (8, 390, 192, 4, 1)])
+@pytest.mark.parametrize("B,cin,cout,H,k", [(4, 48, 54, 16, 3), (4, 54, 48, 16, 5), (4, 96, 96, 8, 5), (2, 192, 192, 8, 3), (8, 390, 192, 4, 1)])
 def test_modconv(ops, B, cin, cout, H, k):
     """Batch-shared modulated conv vs the reference's per-sample grouped conv (generator_13_5.py:234-248)."""
     g = torch.Generator().manual_seed(cin + cout)
