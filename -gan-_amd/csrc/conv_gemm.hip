@@ -1206,6 +1206,7 @@ int tile48() {   // GANAMD_TILE48=0: M = 33..48 on the 64-row tile (A/B)
   return v;
 }
 int conv_bm(int M) {
+  if (M <= 16 && tile48()) return 16;   // ToRGB (M = 3): 16x16x4 blocks halve the empty rows
   if (M <= 32) return 32;
   if (M <= 48 && tile48()) return 48;   // 16x16x4 MFMA blocks: 48 rows without 64-row padding
   if (M <= 64) return 64;
@@ -1218,9 +1219,13 @@ int wide_tiles() {   // GANAMD_WIDE=1: 128 x 256 tiles (2 waves per SIMD) for M 
   static const int v = env_int("GANAMD_WIDE", 0);
   return v;
 }
-int conv_bn(int bm, int) { return bm == 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
+int conv_bn(int bm, int) { return bm <= 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
 int tile96() {   // GANAMD_TILE96=0: wgrad keeps 128-wide tiles on J = 96, 192 (A/B)
   static const int v = env_int("GANAMD_TILE96", 1);
+  return v;
+}
+int big96() {    // GANAMD_BIG96=0: 128x128 wgrad tiles for large M, J that pad them (A/B)
+  static const int v = env_int("GANAMD_BIG96", 1);
   return v;
 }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
@@ -1305,6 +1310,9 @@ int conv_occ() {
 template <int MODE, bool BSCALE, bool BF16>
 int conv_occ_tile(int bm, int bn) {
   switch (bm) {
+    case 16:
+      if constexpr (!BF16) return conv_occ<16, 256, 1, 4, MODE, BSCALE, BF16>();
+      return conv_occ<32, 256, 1, 4, MODE, BSCALE, BF16>();
     case 32: return conv_occ<32, 256, 1, 4, MODE, BSCALE, BF16>();
     case 48:
       if constexpr (!BF16) return conv_occ<48, 128, 1, 4, MODE, BSCALE, BF16>();
@@ -1373,6 +1381,7 @@ ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16
   // the bf16 body has 32x32 blocks only: its 48-row GEMMs run on the 64-row tile over the same
   // 48-row packed operand (rows past it read as 0 through the buffer bound, are not stored)
   if (bf16 && pl.bm == 48) pl.bm = 64;
+  if (bf16 && pl.bm == 16) pl.bm = 32;
   pl.gx = (N + pl.bn - 1) / pl.bn;
   pl.gy = (M + pl.bm - 1) / pl.bm;
   // bf16 kernels take K-steps of BKB = two fp32 steps (conv_body_bf16)
@@ -1446,7 +1455,7 @@ int wgrad_occ() {
 
 template <bool SCALED>
 int wgrad_occ_tile(int bm, int bn) {
-  if (bn == 64) return wgrad_occ<64, 64, 2, 2, SCALED>();
+  if (bn == 64) return bm == 48 ? wgrad_occ<48, 64, 1, 4, SCALED>() : wgrad_occ<64, 64, 2, 2, SCALED>();
   if (bn == 96) return bm == 96 ? wgrad_occ<96, 96, 2, 2, SCALED>() : wgrad_occ<64, 96, 2, 2, SCALED>();
   switch (bm) {
     case 32: return wgrad_occ<32, 128, 1, 4, SCALED>();
@@ -1459,8 +1468,13 @@ int wgrad_occ_tile(int bm, int bn) {
 Plan wgrad_plan(int M, int J, int K, int T, bool scaled, bool bf16) {
   int bm = wgrad_bm(M, scaled), bn = 128;
   if (J <= 64 && bm >= 64) {  // narrow gathered side: a 64x64 tile wastes nothing on J = 48..64
-    bm = 64;
+    bm = (M <= 48 && !bf16 && tile48()) ? 48 : 64;   // 48x64: 16x16x4 blocks, no empty rows at M = 48
     bn = 64;
+  } else if (bm == 128 && !bf16 && tile96() && big96() &&
+             (double)M / ((M + 95) / 96 * 96) * J / ((J + 95) / 96 * 96) >
+                 (double)M / ((M + 127) / 128 * 128) * J / ((J + 127) / 128 * 128) / 0.9) {
+    bm = 96;   // M, J = 1025: 96x96 tiles fill 94 % against 79 % for 128x128
+    bn = 96;
   } else if ((bm == 64 || bm == 96) && !bf16 && tile96() && (J + 95) / 96 * 96 / 0.97 < 0.95 * ((J + 127) / 128 * 128)) {
     bn = 96;   // J = 96, 192, ...: 96-wide tiles (16x16x4 blocks) instead of 25 % empty 128-wide ones
   }
@@ -1587,6 +1601,9 @@ hipError_t launch_conv(ConvArgs p, const ConvPlan& pl, float* slab, hipStream_t 
 template <int MODE, bool BSCALE, bool BF16>
 hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab, hipStream_t st) {
   switch (pl.bm) {
+    case 16:
+      if constexpr (!BF16) return launch_conv<16, 256, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
+      return hipErrorInvalidValue;   // conv_plan moves bf16 to the 32-row tile
     case 32: return launch_conv<32, 256, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
     case 48:
       if constexpr (!BF16) return launch_conv<48, 128, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
@@ -1772,7 +1789,11 @@ hipError_t launch_wgrad(WgradArgs p, int T, const Plan& pl, float* slab, hipStre
 
 template <int MODE, bool SCALED, bool BF16>
 hipError_t dispatch_wgrad_tile(const WgradArgs& p, int T, const Plan& pl, float* slab, hipStream_t st) {
-  if (pl.bn == 64) return launch_wgrad<64, 64, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
+  if (pl.bn == 64) {
+    if constexpr (!BF16)
+      if (pl.bm == 48) return launch_wgrad<48, 64, 1, 4, MODE, SCALED, BF16>(p, T, pl, slab, st);
+    return launch_wgrad<64, 64, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st);
+  }
   if (pl.bn == 96) {   // 16x16x4 blocks: fp32 only (wgrad_plan gives bf16 128-wide tiles)
     if constexpr (!BF16)
       return pl.bm == 96 ? launch_wgrad<96, 96, 2, 2, MODE, SCALED, BF16>(p, T, pl, slab, st)

@@ -19,6 +19,10 @@ SHAPES_WGRAD = [
     ("wgrad", 64, 192, 16, 192, 5, 1, 2, True, 10),
     ("wgrad", 128, 3, 64, 64, 3, 1, 1, False, 5),
     ("wgrad", 64, 96, 32, 96, 3, 1, 1, True, 30),
+    ("wgrad", 64, 1025, 4, 1025, 3, 1, 1, False, 60),
+    ("wgrad", 128, 1025, 4, 1025, 3, 1, 1, False, 30),
+    ("fwd", 64, 108, 64, 3, 5, 1, 2, False, 12),
+    ("dgrad", 64, 48, 64, 48, 5, 1, 2, True, 20),
 ]
 SHAPES = [  # (op, B, cin, H, cout, k, stride, pad, scaled, weight = launches per iteration)
     ("fwd", 64, 96, 64, 96, 5, 1, 2, True, 60),
