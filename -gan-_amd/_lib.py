@@ -96,6 +96,8 @@ _SIGS = {
     "ganamd_mbstd_bwd": (c_int, [vp, c_long, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, vp]),
     "ganamd_mbstd_tangent": (c_int, [vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, vp]),
     "ganamd_mbstd_adjoint": (c_int, [vp, vp, c_long, vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, vp]),
+    "ganamd_linear_bn_act": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp, vp, vp, c_float, c_float,
+                                     vp, vp, vp]),
     "ganamd_philox_uniform": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_normal": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_image_batch_workspace": (c_size_t, [c_int, c_int, c_int]),

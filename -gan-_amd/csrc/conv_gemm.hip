@@ -1648,10 +1648,26 @@ hipError_t dispatch_conv_mode(const ConvArgs& p, const ConvPlan& pl, float* slab
 // through LDS before the conv epilogue (alpha, scale, bias, PReLU).  No slab, no second launch.
 constexpr int LBM = 32;
 
+// Train-mode BatchNorm1d (+ PReLU) fused into the linear's epilogue (ganamd_linear_bn_act): the
+// block owns whole rows (N <= 64 columns = one wave), so the batch statistics are wave sums.
+struct BNArgs {
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // JT: 32-column MFMA tiles per block (2: N <= 64, 4: 128 columns); NW waves split K; chunks of 16 k
 // are loaded four at a time (four in flight per wave) before their MFMAs.
-template <int JT, int NW>
-__global__ __launch_bounds__(64 * NW) void linear_gemm_kernel(ConvArgs p) {
+template <int JT, int NW, bool BN = false>
+__global__ __launch_bounds__(64 * NW) void linear_gemm_kernel(ConvArgs p, BNArgs bn) {
   constexpr int LBN = 32 * JT;
   __shared__ __attribute__((aligned(16))) float red[NW][LBM * LBN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1712,6 +1728,36 @@ __global__ __launch_bounds__(64 * NW) void linear_gemm_kernel(ConvArgs p) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) red[wave][((e & 3) + 8 * (e >> 2) + 4 * h) * LBN + 32 * j + r] = acc[j][e];
   __syncthreads();
+  if constexpr (BN) {
+    // rows wave + NW*q, one column per lane: y = act(gamma (v - mean) / sqrt(var + eps) + beta)
+    // with the batch mean / biased variance of the row; running stats take the unbiased variance
+    static_assert(LBN == 64 && LBM % NW == 0, "BN epilogue: one wave per 64-column row");
+    const float inv_n = 1.f / (float)N;
+    for (int row = wave; row < LBM; row += NW) {
+      const int m = m0 + row;
+      if (m >= p.M) break;                         // wave-uniform
+      const bool ok = lane < N;
+      float v = 0.f;
+      if (ok) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) v += red[w][row * LBN + lane];
+        v *= p.alpha;
+        if (p.bias) v += p.bias[m];
+      }
+      const float mean = wave_sum(v) * inv_n;
+      const float d = ok ? v - mean : 0.f;
+      const float var = wave_sum(d * d) * inv_n;
+      float yv = d * (1.f / sqrtf(var + bn.eps)) * bn.gamma[m] + bn.beta[m];
+      if (p.act) yv = yv > 0.f ? yv : p.act[m] * yv;
+      if (ok) p.y[(long)m * p.ldy + lane] = yv;
+      if (lane == 0) {
+        const float mo = bn.momentum;
+        bn.running_mean[m] = (1.f - mo) * bn.running_mean[m] + mo * mean;
+        bn.running_var[m] = (1.f - mo) * bn.running_var[m] + mo * var * ((float)N / (float)(N - 1));
+      }
+    }
+    return;
+  }
   for (int idx = tid; idx < LBM * LBN; idx += 64 * NW) {
     const int row = idx / LBN, col = idx - row * LBN;
     const int m = m0 + row, n = n0 + col;
@@ -1738,9 +1784,10 @@ bool linear_ok(const ConvArgs& p) {
 
 hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
   if (p.N <= 64)
-    hipLaunchKernelGGL((linear_gemm_kernel<2, 8>), dim3((p.M + LBM - 1) / LBM, 1), dim3(512), 0, st, p);
+    hipLaunchKernelGGL((linear_gemm_kernel<2, 8>), dim3((p.M + LBM - 1) / LBM, 1), dim3(512), 0, st, p, BNArgs{});
   else
-    hipLaunchKernelGGL((linear_gemm_kernel<4, 4>), dim3((p.M + LBM - 1) / LBM, (p.N + 127) / 128), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((linear_gemm_kernel<4, 4>), dim3((p.M + LBM - 1) / LBM, (p.N + 127) / 128), dim3(256), 0, st, p,
+                       BNArgs{});
   return hipGetLastError();
 }
 
@@ -2042,6 +2089,48 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
                     hipStream_t stream) {
   return ganamd_conv_fwd_ex(d, x, w, bias, x_scale, y_scale, alpha, nullptr, nullptr, nullptr, y, workspace, stream);
+}
+
+int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias, float alpha,
+                         const float* gamma, const float* beta, const float* act_alpha, float* running_mean,
+                         float* running_var, float momentum, float eps, float* y, void* workspace,
+                         hipStream_t stream) {
+  if (!desc_ok(d) || !x || !w || !y || !gamma || !beta || !running_mean || !running_var) return GANAMD_EINVAL;
+  if (d->H != 1 || d->W != 1 || d->KH != 1 || d->KW != 1 || d->transposed || d->stride != 1 || d->pad != 0 ||
+      d->math != GANAMD_MATH_F32 || d->B < 2 || d->B > 64)
+    return GANAMD_EINVAL;
+  size_t need = 0;
+  ganamd_conv_workspace(d, GANAMD_CONV_FWD, &need);
+  if (need && !d->packed_w && !workspace) return GANAMD_EINVAL;
+  ConvArgs p{};
+  p.M = d->Cout;
+  p.Ck = d->Cin;
+  p.T = 1;
+  p.sm = d->Cin;
+  p.sc = 1;
+  p.st = 1;
+  p.g = Gather{x, nullptr, d->Cin, d->B, 1, 1, 1, 1, 1, 1, 0, kZero};
+  p.y = y;
+  p.bias = bias;
+  p.act = act_alpha;
+  p.alpha = alpha;
+  p.N = d->B;
+  p.ohw = 1;
+  p.ldy = d->B;
+  const int bmp = conv_bm(p.M);
+  const int mpad = (p.M + bmp - 1) / bmp * bmp;
+  p.Ckp = (p.Ck + BK - 1) / BK * BK;
+  if (!linear_ok(p)) return GANAMD_EINVAL;     // the skinny-GEMM domain (M x K <= 4 M weights)
+  p.w = w;
+  if (!d->packed_w) {
+    float* packed = static_cast<float*>(workspace);
+    launch_pack(ganamd_pack_job{w, packed, p.sm, p.sc, p.st, p.M, p.Ck, 1, mpad, p.Ckp, 1, 0, 0, 0}, stream);
+    p.w = packed;
+  }
+  p.w_bytes = 4 * mpad * p.Ckp;
+  hipLaunchKernelGGL((linear_gemm_kernel<2, 8, true>), dim3((p.M + LBM - 1) / LBM, 1), dim3(512), 0, stream, p,
+                     BNArgs{gamma, beta, running_mean, running_var, momentum, eps});
+  return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,

@@ -73,6 +73,9 @@ def _conv_bn_act(conv, bn, act, x):
 
 
 def _lin_bn_act(lin, bn, act, x):
+    # no-grad forwards (the critic steps' fake batches): linear + BatchNorm1d + PReLU in one launch
+    if ops.linear_bn_act_ok(x, lin.weight.weights):
+        return ops.linear_bn_act(x, lin.weight.weights, lin.bias, lin.weight.scale, bn, act)
     return bn_act(lin(x), bn, act)
 
 
@@ -237,7 +240,7 @@ class Conv2dWeightModulate(nn.Module):
         if self._bank_sd is not None:
             s, d = self._bank_sd
         else:
-            s = bn_act(self.to_style[1](self.to_style[0](w)), self.to_style[2], None)   # [Cin, B]
+            s = _lin_bn_act(self.to_style[1], self.to_style[2], None, self.to_style[0](w))   # [Cin, B]
             d = ops.demod(s, self.weight.weights, self.weight.scale)
         if not torch.is_grad_enabled():
             return ops.modconv_fused(x, s, d, self.weight.weights, geo, self.weight.scale, noise, noise_scale, act)
@@ -381,7 +384,7 @@ class SEBlock_conv(nn.Module):
         t = _conv_bn_act(c[0], c[1], c[2], ops.resample(x, "pool5"))
         t = _conv_bn_act(c[3], c[4], c[5], t)
         z = _lin_bn_act(self.fcs[0], self.fcs[1], self.fcs[2], ops.plane_mean(t))
-        return ops.sigmoid(bn_act(self.fc_out(z), self.fc_bn, None))
+        return ops.sigmoid(_lin_bn_act(self.fc_out, self.fc_bn, None, z))
 
 
 class SEBlock_fc(nn.Module):
@@ -400,7 +403,7 @@ class SEBlock_fc(nn.Module):
         f = self.fcs
         z = _lin_bn_act(f[0], f[1], f[2], ops.plane_mean(x))
         z = _lin_bn_act(f[3], f[4], f[5], z)
-        return ops.sigmoid(bn_act(self.fc_out(z), self.fc_bn, None))
+        return ops.sigmoid(_lin_bn_act(self.fc_out, self.fc_bn, None, z))
 
 
 class BasicBlock(nn.Module):

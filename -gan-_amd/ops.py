@@ -657,6 +657,38 @@ class BNAct(Function):
         return gx, gg, gb, ga, None, None, None, None
 
 
+def linear_bn_act_ok(x, w) -> bool:
+    """Whether ``linear_bn_act`` takes this linear: no autograd, fp32 math (bf16 mode keeps its bf16
+    linears), [Cin, B] with 2 <= B <= 64 and at most 4 M weights (ganamd_linear_bn_act's domain)."""
+    return (not torch.is_grad_enabled() and _MATH[0] == _lib.MATH_F32 and x.dim() == 2 and 2 <= x.shape[1] <= 64
+            and w.shape[0] * w.shape[1] <= (4 << 20))
+
+
+def linear_bn_act(x, w, bias, alpha: float, bn, act=None):
+    """``act(bn(linear(x)))`` in train mode as ONE kernel (no-grad forward only, see linear_bn_act_ok):
+    the linear's epilogue computes each row's batch statistics (ganamd_linear_bn_act)."""
+    cin, B = x.shape
+    cout = w.shape[0]
+    geo = linear_geo(B, cin, cout)
+    x = _c(x)
+    for t, n, nm in ((bias, cout, "bias"), (bn.weight, cout, "gamma"), (bn.bias, cout, "beta"),
+                     (bn.running_mean, cout, "running_mean"), (bn.running_var, cout, "running_var"),
+                     (None if act is None else act.weight, cout, "prelu alpha")):
+        _need(t, n, f"linear_bn_act {nm}")
+    FlopCounter.add(geo, "fwd", False, False)
+    y = torch.empty((cout, B), device=x.device, dtype=torch.float32)
+    wv = w.reshape(cout, cin, 1, 1)
+    pw = PackCache.get(geo, _lib.CONV_FWD, wv)
+    packed = pw is not None
+    nb = geo.ws_bytes(_lib.CONV_FWD, packed)
+    ws = workspace(nb, x.device) if (nb and not packed) else None
+    check(LIB.ganamd_linear_bn_act(geo.desc(packed), ptr(x), ptr(pw if packed else wv), ptr(bias), float(alpha),
+                                   ptr(bn.weight), ptr(bn.bias), ptr(None if act is None else act.weight),
+                                   ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum), float(bn.eps),
+                                   ptr(y), ptr(ws), stream()), "linear_bn_act")
+    return y
+
+
 def bn_act(x, bn: torch.nn.modules.batchnorm._BatchNorm, act: torch.nn.PReLU | None = None):
     """Train-mode ``act(bn(x))`` with the module's parameters and running buffers."""
     return BNAct.apply(x, bn.weight, bn.bias, None if act is None else act.weight, bn.running_mean, bn.running_var,

@@ -331,6 +331,21 @@ int ganamd_mbstd_adjoint(const float* x, const float* xd, long ldx, const float*
                          int B, int HW, int S, int G, float* ax, void* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Linear + train-mode BatchNorm1d (+ PReLU) in one launch, the generator's
+ * EqualizedLinear -> BatchNorm1d -> PReLU chains (SK attention fc / heads, SE fc, mapping MLPs;
+ * generators/generator_13_5.py:19-26, 48-50, 71-79) on feature-major [Cin][B] activations:
+ *   v = alpha * W x + bias;  y = act(gamma * (v - mean_b v) / sqrt(var_b v + eps) + beta)
+ * with the batch mean and biased variance of each output row; running_mean / running_var
+ * updated in place with momentum (unbiased variance), as torch.nn.BatchNorm1d in train mode.
+ * The block owns whole rows: 2 <= B <= 64, Cout * Cin <= 4 M, fp32, 1x1 geometry (H = W = 1).
+ * Workspace: ganamd_conv_workspace(d, GANAMD_CONV_FWD) bytes unless d->packed_w.
+ * ------------------------------------------------------------------------------------- */
+int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias, float alpha,
+                         const float* gamma, const float* beta, const float* act_alpha, float* running_mean,
+                         float* running_var, float momentum, float eps, float* y, void* workspace,
+                         hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Device random numbers (Philox4x32-10) for z, eps and the StyleConv noise.
  * Replaces torch.randn / torch.rand on the path (train/wgangp.py:22,35,58;
  * generator_13_5.py:265; train/gan.py:21,32 label noise).  Element 4g+i of a draw is word i of

@@ -583,3 +583,41 @@ def test_grad_penalty_fused(ops, mode, center, lam):
     assert abs(float(out) - float(ref)) / abs(float(ref)) < 1e-6
     (got,) = torch.autograd.grad(out * 0.7, g)
     assert rel(got, want) < 1e-6
+
+
+@pytest.mark.parametrize("B,cin,cout,act", [(4, 48, 48, True), (64, 192, 192, True), (37, 384, 96, False),
+                                            (64, 1025, 256, True), (2, 96, 40, True)])
+def test_linear_bn_act_fused(ops, B, cin, cout, act):
+    """ganamd_linear_bn_act (no-grad: linear + train-mode BatchNorm1d + PReLU in one launch) against
+    the float64 torch composition; running statistics updated as torch's BatchNorm1d does."""
+    g = torch.Generator().manual_seed(B + cin + cout)
+    x = torch.randn(cin, B, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, generator=g, dtype=torch.float64)
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    alpha = 1.0 / cin ** 0.5
+    bn = torch.nn.BatchNorm1d(cout).double()
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(cout, generator=g, dtype=torch.float64))
+        bn.bias.copy_(0.1 * torch.randn(cout, generator=g, dtype=torch.float64))
+        bn.running_mean.copy_(0.2 * torch.randn(cout, generator=g, dtype=torch.float64))
+        bn.running_var.copy_(1 + 0.2 * torch.rand(cout, generator=g, dtype=torch.float64))
+    pr = torch.nn.PReLU(cout).double() if act else None
+    if pr is not None:
+        with torch.no_grad():
+            pr.weight.copy_(0.25 + 0.1 * torch.randn(cout, generator=g, dtype=torch.float64))
+    bn_g = torch.nn.BatchNorm1d(cout).to(DEV)
+    bn_g.load_state_dict({k: v.float() for k, v in bn.state_dict().items()})
+    pr_g = None
+    if pr is not None:
+        pr_g = torch.nn.PReLU(cout).to(DEV)
+        pr_g.load_state_dict({k: v.float() for k, v in pr.state_dict().items()})
+    w_g = torch.nn.Parameter(w.float().to(DEV))
+    with torch.no_grad():
+        ref = bn((alpha * x.t() @ w.t() + b))          # [B, cout], updates bn's running stats
+        if pr is not None:
+            ref = pr(ref)
+        assert ops.linear_bn_act_ok(x.float().to(DEV), w_g)
+        y = ops.linear_bn_act(x.float().to(DEV), w_g, b.float().to(DEV), alpha, bn_g, pr_g)
+    assert rel(y.t(), ref) < 1e-5
+    assert rel(bn_g.running_mean, bn.running_mean) < 1e-5
+    assert rel(bn_g.running_var, bn.running_var) < 1e-5

@@ -21,15 +21,5 @@ timeout -k 10 900 rocprofv3 --kernel-trace -d /tmp/prof_${R}b -o run --output-fo
 T2=$(find /tmp/prof_${R}b -name "*kernel_trace.csv")
 MS2=$(python3 -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]['ms_per_step'])" gpurun_out/${R}_bench_prof2.log)
 python3 tools/trace_summary.py "$T2" --last $(python3 -c "print($MS2/1000*0.98)") --top 60 > gpurun_out/${R}_iteration_summary.txt
-python3 - "$T" > gpurun_out/${R}_roofline_probe.txt <<'PY'
-import csv, sys
-# the probe's launches: that kernel at 768 whole-tile blocks (Grid_Size_X = 768 * 256 threads)
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_gemm_kernel<128, 128, 2, 2, 1, false, false>" in r["Kernel_Name"]
-        and int(r["Grid_Size_X"]) == 768 * 256]
-rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-last = rows[-20:]
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
-print(f"roofline probe: last {len(d)} dispatches of conv_gemm_kernel<128,128,2,2,1,false,false> at 768 blocks in the bench trace")
-print(f"average {sum(d) / len(d):.1f} us  min {min(d):.1f}  max {max(d):.1f}")
-PY
+python3 tools/probe_from_trace.py "$T" > gpurun_out/${R}_roofline_probe.txt
 timeout -k 10 900 python3 bench.py > gpurun_out/${R}_bench.log 2>&1
