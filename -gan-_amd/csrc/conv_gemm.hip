@@ -132,13 +132,46 @@ __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int k
 
 // Output column of GEMM column n: the identity, or for one phase (qh, qw) of a stride-s transposed
 // conv n = (b, j, i) over the OHp x OWp phase grid -> (b, s*j + qh, s*i + qw) of the OH x OW output.
+//
+// s = -1 (frame split, the stride-1 dgrad): n = (b, a, c) over the (H+2p) x (W+2p) padded input
+// frame (ohwp = its size, OWp = its width, OW = W, OHW = H*W, qh = p, qw = H); interior positions
+// go straight to the input gradient, ring positions to `ring` ([row][b][Rn], Rn ring positions
+// per image, row stride ldr) -- dropped for zero padding (ring = null), folded onto the edge
+// pixels by ring_fold_kernel for replication padding.  No frame buffer, no full fold pass.
 struct OutMap {
   int s, qh, qw, OWp, ohwp, OW, OHW;
+  int Rn;
+  long ldr;
+  float* ring;
 };
 __device__ __forceinline__ long out_col(const OutMap& r, int n) {
   if (r.s == 0) return n;
   const int b = n / r.ohwp, q = n - b * r.ohwp, j = q / r.OWp, i = q - j * r.OWp;
   return (long)b * r.OHW + (long)(r.s * j + r.qh) * r.OW + r.s * i + r.qw;
+}
+// ring position index of frame point (a, c) (not interior): top rows, bottom rows, then the
+// 2p side columns of the H middle rows
+__host__ __device__ __forceinline__ int ring_idx(int a, int c, int p, int H, int W, int Wp) {
+  if (a < p) return a * Wp + c;
+  if (a >= p + H) return (a - H) * Wp + c;
+  return 2 * p * Wp + (a - p) * 2 * p + (c < p ? c : c - W);
+}
+// frame split: destination (base, row stride, column) of GEMM column n; false = not stored
+__device__ __forceinline__ bool frame_target(const OutMap& r, float* y, long ldy, int n, float*& base, long& ld,
+                                             long& col) {
+  const int p = r.qh, H = r.qw, W = r.OW;
+  const int b = n / r.ohwp, q = n - b * r.ohwp, a = q / r.OWp, c = q - a * r.OWp;
+  if (a >= p && a < p + H && c >= p && c < p + W) {
+    base = y;
+    ld = ldy;
+    col = (long)b * r.OHW + (long)(a - p) * W + (c - p);
+    return true;
+  }
+  if (!r.ring) return false;
+  base = r.ring;
+  ld = r.ldr;
+  col = (long)b * r.Rn + ring_idx(a, c, p, H, W, r.OWp);
+  return true;
 }
 
 struct ConvArgs {
@@ -565,7 +598,13 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
     const int n = n0 + (wn * C::TN + j) * 32 + (lane & 31);
     if (n >= p.N) continue;
     const int b = (finish && p.oscale) ? n / p.ohw : 0;
-    const long col = (MODE == kPhase && finish) ? out_col(p.om, n) : n;
+    float* obase = out;
+    long old = ldo, col = n;
+    if (finish) {
+      if constexpr (MODE == kPhase) col = out_col(p.om, n);
+      if constexpr (MODE == kTransposed)
+        if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) continue;
+    }
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
@@ -579,7 +618,7 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
           if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
           if (p.act) v = v > 0.f ? v : p.act[m] * v;
         }
-        out[(long)m * ldo + col] = v;
+        obase[(long)m * old + col] = v;
       }
     }
   }
@@ -793,7 +832,13 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
     const int n = n0 + (wn * C::TN + j) * C::MB + (lane & (C::MB - 1));
     if (n >= p.N) continue;
     const int b = (finish && p.oscale) ? n / p.ohw : 0;
-    const long col = (MODE == kPhase && finish) ? out_col(p.om, n) : n;
+    float* obase = out;
+    long old = ldo, col = n;
+    if (finish) {
+      if constexpr (MODE == kPhase) col = out_col(p.om, n);
+      if constexpr (MODE == kTransposed)
+        if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) continue;
+    }
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
 #pragma unroll
@@ -807,7 +852,7 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
           if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
           if (p.act) v = v > 0.f ? v : p.act[m] * v;
         }
-        out[(long)m * ldo + col] = v;
+        obase[(long)m * old + col] = v;
       }
     }
   }
@@ -1089,30 +1134,41 @@ void wgrad_gemm_kernel(WgradArgs p) {
   }
 }
 
-// Sum the replication-padded dgrad image back onto the edge pixels (ReplicationPad2d backward),
-// or crop it for zero padding.  xp: [C*B][Hp][Wp] -> x: [C*B][H][W].
-// I: index type (32-bit whenever the tensor allows it: 64-bit division is a long software sequence).
-template <typename I>
-__global__ void fold_pad_kernel(const float* __restrict__ xp, float* __restrict__ x, long planes, int H, int W,
-                                int pad, int replicate) {
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  const I total = (I)(planes * H * W);
-  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
-    const I r = i / (I)W;
-    const int w = (int)(i - r * (I)W);
-    const I pl = r / (I)H;
-    const int h = (int)(r - pl * (I)H);
-    const float* s = xp + (long)pl * Hp * Wp;
-    if (!replicate) {
-      x[i] = s[(h + pad) * Wp + (w + pad)];
-      continue;
+// Replication padding's adjoint on the ring of the frame-split dgrad (OutMap s = -1): every edge
+// pixel of the input gradient adds the ring positions of the padded frame that clamp onto it
+// (its interior position went to gx directly).  One thread per (plane, edge pixel): top row,
+// bottom row, then the left and right columns of the middle rows.
+__global__ void ring_fold_kernel(const float* __restrict__ ring, float* __restrict__ gx, int planes, int H, int W,
+                                 int p) {
+  const int Hp = H + 2 * p, Wp = W + 2 * p, Rn = Hp * Wp - H * W;
+  const int mid = H > 2 ? H - 2 : 0;
+  const int e_top = W, e_bot = H > 1 ? W : 0, e_right = W > 1 ? mid : 0;
+  const int E = e_top + e_bot + mid + e_right;
+  const long total = (long)planes * E;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int pl = (int)(idx / E), e = (int)(idx - (long)pl * E);
+    int i, j;
+    if (e < e_top) {
+      i = 0;
+      j = e;
+    } else if (e < e_top + e_bot) {
+      i = H - 1;
+      j = e - e_top;
+    } else if (e < e_top + e_bot + mid) {
+      i = 1 + (e - e_top - e_bot);
+      j = 0;
+    } else {
+      i = 1 + (e - e_top - e_bot - mid);
+      j = W - 1;
     }
-    const int h0 = h == 0 ? 0 : h + pad, h1 = h == H - 1 ? Hp - 1 : h + pad;
-    const int w0 = w == 0 ? 0 : w + pad, w1 = w == W - 1 ? Wp - 1 : w + pad;
+    const int h0 = i == 0 ? 0 : i + p, h1 = i == H - 1 ? Hp - 1 : i + p;
+    const int w0 = j == 0 ? 0 : j + p, w1 = j == W - 1 ? Wp - 1 : j + p;
+    const float* r = ring + (long)pl * Rn;
     float acc = 0.f;
     for (int a = h0; a <= h1; ++a)
-      for (int c = w0; c <= w1; ++c) acc += s[a * Wp + c];
-    x[i] = acc;
+      for (int c = w0; c <= w1; ++c)
+        if (a != i + p || c != j + p) acc += r[ring_idx(a, c, p, H, W, Wp)];
+    gx[(long)pl * H * W + (long)i * W + j] += acc;
   }
 }
 
@@ -1516,7 +1572,15 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(
       v[0] = a;
     }
     const int n = n0 + (int)c;
-    const long o = (long)m * ldy + out_col(om, n);   // VEC: om is the identity, o .. o + 3 contiguous
+    float* yb = y;
+    long o;
+    if (!VEC && om.s < 0) {   // frame split (stride-1 dgrad): interior -> y, ring -> om.ring
+      long ld, col;
+      if (!frame_target(om, y, ldy, n, yb, ld, col)) continue;
+      o = (long)m * ld + col;
+    } else {
+      o = (long)m * ldy + out_col(om, n);   // VEC: om is the identity, o .. o + 3 contiguous
+    }
     const float bm = bias ? bias[m] : 0.f, ns = noise ? noise_scale[m] : 0.f, am = act ? act[m] : 1.f;
     float nz[V];
     if (noise) {
@@ -1537,9 +1601,9 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(
       v[q] = r;
     }
     if constexpr (VEC) {
-      *reinterpret_cast<f32x4*>(y + o) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(yb + o) = f32x4{v[0], v[1], v[2], v[3]};
     } else {
-      y[o] = v[0];
+      yb[o] = v[0];
     }
   }
 }
@@ -1988,9 +2052,11 @@ static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* 
                          ph ? d->stride : 1, ph ? d->KH : 0, ph ? d->pad : 0, 0};
 }
 
+// The frame-split dgrad's ring buffer (replication padding only: zero padding drops the ring)
 static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
-  if (d->transposed || d->pad == 0 || dgrad_scatter(d)) return 0;
-  return sizeof(float) * (size_t)d->Cin * d->B * (d->H + 2 * d->pad) * (d->W + 2 * d->pad);
+  if (d->transposed || d->pad == 0 || dgrad_scatter(d) || d->pad_mode != GANAMD_PAD_REPLICATE) return 0;
+  const size_t Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
+  return sizeof(float) * (size_t)d->Cin * d->B * (Hp * Wp - (size_t)d->H * d->W);
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -2249,23 +2315,25 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     p.ohw = d->H * d->W;
     return dispatch_conv(p, pre, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
-  // dX of conv = transposed gather of gy into the padded input frame, then fold the pad
+  // dX of conv = transposed gather of gy over the padded input frame.  Padded convs split the
+  // frame in the epilogue (OutMap s = -1): interior -> gx, ring -> ring buffer (replication) or
+  // dropped (zero padding); ring_fold_kernel then adds the ring onto the edge pixels.
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
-  float* out = pad_bytes ? reinterpret_cast<float*>(ws) : gx;
   p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
-  p.y = out;
+  p.y = gx;
   p.ohw = Hp * Wp;
+  float* ring = pad_bytes ? reinterpret_cast<float*>(ws) : nullptr;
+  const int Rn = Hp * Wp - d->H * d->W;
+  if (d->pad > 0) {
+    p.om = OutMap{-1, d->pad, d->H, Wp, Hp * Wp, d->W, d->H * d->W, Rn, (long)d->B * Rn, ring};
+    p.ldy = (long)d->B * d->H * d->W;
+  }
   if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
-  if (pad_bytes) {
+  if (ring) {
     const long planes = (long)d->Cin * d->B;
-    const long total = planes * d->H * d->W;
-    const int rep = d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0;
-    if (total < (1L << 31) - (1L << 24))
-      hipLaunchKernelGGL(fold_pad_kernel<unsigned>, dim3(grid1d(total)), dim3(256), 0, stream, out, gx, planes, d->H,
-                         d->W, d->pad, rep);
-    else
-      hipLaunchKernelGGL(fold_pad_kernel<long>, dim3(grid1d(total)), dim3(256), 0, stream, out, gx, planes, d->H, d->W,
-                         d->pad, rep);
+    const long edges = (long)2 * d->W + 2 * d->H;
+    hipLaunchKernelGGL(ring_fold_kernel, dim3(grid1d(planes * edges)), dim3(256), 0, stream, ring, gx, (int)planes,
+                       d->H, d->W, d->pad);
     if (hipGetLastError() != hipSuccess) return GANAMD_ELAUNCH;
   }
   return GANAMD_OK;
