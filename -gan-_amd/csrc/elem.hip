@@ -234,6 +234,105 @@ __global__ __launch_bounds__(kNT) void bn_small_bwd_kernel(const float* __restri
   }
 }
 
+// Medium rows (the 4x4 .. 8x8 and 5x5-pool maps of the SK-attention / SE convs: 512 < L <= 8192):
+// one block per row, the row held in registers (32 values per thread), double block sums --
+// statistics + normalisation + PReLU (and the backward) in ONE launch instead of partial + apply.
+constexpr int kMidL = 8192;
+constexpr int kMidPer = kMidL / kNT;
+
+__global__ __launch_bounds__(kNT) void bn_mid_fwd_kernel(const float* __restrict__ x, int L,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         const float* __restrict__ alpha, float* running_mean,
+                                                         float* running_var, float momentum, float eps,
+                                                         float* __restrict__ y, float* __restrict__ save_mean,
+                                                         float* __restrict__ save_invstd) {
+  __shared__ double sh[kNT / 64];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float* row = x + (long)c * L;
+  float v[kMidPer];
+  double sum = 0.0;
+#pragma unroll
+  for (int j = 0; j < kMidPer; ++j) {
+    const int i = tid + kNT * j;
+    v[j] = i < L ? row[i] : 0.f;
+    sum += v[j];
+  }
+  const double mean = block_sum_d(sum, sh) / L;
+  double m2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < kMidPer; ++j) {
+    const double d = v[j] - mean;
+    if (tid + kNT * j < L) m2 += d * d;
+  }
+  m2 = block_sum_d(m2, sh);
+  const float mu = (float)mean, is = (float)(1.0 / sqrt(m2 / L + (double)eps));
+  if (tid == 0) bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
+  const float ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  float* yr = y + (long)c * L;
+#pragma unroll
+  for (int j = 0; j < kMidPer; ++j) {
+    const int i = tid + kNT * j;
+    if (i < L) {
+      float z = (v[j] - mu) * is * ga + be;
+      if (alpha) z = z > 0.f ? z : al * z;
+      yr[i] = z;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kNT) void bn_mid_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                                                         int L, const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         const float* __restrict__ alpha, float* __restrict__ gx,
+                                                         float* __restrict__ ggamma, float* __restrict__ gbeta,
+                                                         float* __restrict__ galpha, int accumulate) {
+  __shared__ double sh[kNT / 64];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  const float* xr = x + (long)c * L;
+  const float* gr = gy + (long)c * L;
+  float xh[kMidPer], g[kMidPer];
+  double sg = 0.0, sgx = 0.0, sa = 0.0;
+#pragma unroll
+  for (int j = 0; j < kMidPer; ++j) {
+    const int i = tid + kNT * j;
+    xh[j] = 0.f;
+    g[j] = 0.f;
+    if (i < L) {
+      xh[j] = (xr[i] - mu) * is;
+      const float gv = gr[i];
+      g[j] = gv;
+      if (alpha) {
+        const float z = xh[j] * ga + be;
+        if (!(z > 0.f)) {
+          g[j] = gv * al;
+          sa += (double)gv * z;
+        }
+      }
+      sg += g[j];
+      sgx += (double)g[j] * xh[j];
+    }
+  }
+  sg = block_sum_d(sg, sh);
+  sgx = block_sum_d(sgx, sh);
+  if (alpha) sa = block_sum_d(sa, sh);
+  if (tid == 0) {
+    gbeta[c] = accumulate ? gbeta[c] + (float)sg : (float)sg;
+    ggamma[c] = accumulate ? ggamma[c] + (float)sgx : (float)sgx;
+    if (alpha && galpha) galpha[c] = accumulate ? galpha[c] + (float)sa : (float)sa;
+  }
+  const float mg = (float)(sg / L), mgx = (float)(sgx / L), k = ga * is;
+  float* gxr = gx + (long)c * L;
+#pragma unroll
+  for (int j = 0; j < kMidPer; ++j) {
+    const int i = tid + kNT * j;
+    if (i < L) gxr[i] = k * (g[j] - mg - xh[j] * mgx);
+  }
+}
+
 __global__ __launch_bounds__(kNT) void bn_act_apply_kernel(const float* __restrict__ x, int C, long L,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -747,6 +846,11 @@ int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const f
                        running_mean, running_var, momentum, eps, y, save_mean, save_invstd);
     return ok(hipGetLastError());
   }
+  if (L <= kMidL) {
+    hipLaunchKernelGGL(bn_mid_fwd_kernel, dim3(C), dim3(kNT), 0, st, x, (int)L, gamma, beta, alpha, running_mean,
+                       running_var, momentum, eps, y, save_mean, save_invstd);
+    return ok(hipGetLastError());
+  }
   const int S = splits_for(L);
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_partial_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part);
@@ -763,6 +867,11 @@ int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const floa
   if (L <= kSmallL) {
     hipLaunchKernelGGL(bn_small_bwd_kernel, dim3((C + 3) / 4), dim3(kNT), 0, st, gy, x, C, (int)L, save_mean,
                        save_invstd, gamma, beta, alpha, gx, ggamma, gbeta, galpha, accumulate);
+    return ok(hipGetLastError());
+  }
+  if (L <= kMidL) {
+    hipLaunchKernelGGL(bn_mid_bwd_kernel, dim3(C), dim3(kNT), 0, st, gy, x, (int)L, save_mean, save_invstd, gamma,
+                       beta, alpha, gx, ggamma, gbeta, galpha, accumulate);
     return ok(hipGetLastError());
   }
   const int S = splits_for(L);

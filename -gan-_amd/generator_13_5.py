@@ -85,6 +85,13 @@ def _mix(feas, att):
 
 
 def _heads(attn, z):
+    if not torch.is_grad_enabled():   # each head's last linear writes its slice of [M, C, B] (no stack copy)
+        out = torch.empty((attn.M,) + tuple(z.shape), device=z.device, dtype=torch.float32)
+        for i in range(attn.M):
+            sub = getattr(attn, f"fc_sub_{i}")
+            v = _lin_bn_act(sub[0], sub[1], sub[2], z)
+            ops.linear(v, sub[3].weight.weights, sub[3].bias, sub[3].weight.scale, out=out[i])
+        return ops.softmax_m(out)
     vecs = []
     for i in range(attn.M):
         sub = getattr(attn, f"fc_sub_{i}")

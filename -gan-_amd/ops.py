@@ -311,14 +311,17 @@ def _w_numel(geo):
     return geo.Cin * geo.Cout * geo.K * geo.K
 
 
-def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0):
+def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0, out=None):
     _need(x, geo.Cin * geo.B * geo.H * geo.W, "conv_fwd x")
     _need(w, _w_numel(geo), "conv_fwd w")
     _need(bias, geo.Cout, "conv_fwd bias")
     _need(xs, geo.Cin * geo.B, "conv_fwd x_scale")
     _need(ys, geo.Cout * geo.B, "conv_fwd y_scale")
     FlopCounter.add(geo, "fwd", xs is not None, ys is not None)
-    y = torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device, dtype=torch.float32)
+    if out is not None:
+        _need(out, geo.Cout * geo.B * geo.OH * geo.OW, "conv_fwd out")
+    y = out if out is not None else torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device,
+                                                dtype=torch.float32)
     pw = PackCache.get(geo, _lib.CONV_FWD, w)
     packed = pw is not None
     nb = geo.ws_bytes(_lib.CONV_FWD, packed)
@@ -485,11 +488,17 @@ def conv2d(x, w, bias, geo: Geo, alpha: float):
     return ConvFwd.apply(x, w, bias, geo, alpha)
 
 
-def linear(x, w, bias, alpha: float):
-    """EqualizedLinear on [Cin, B] -> [Cout, B] (a 1x1 conv at H = W = 1)."""
+def linear(x, w, bias, alpha: float, out=None):
+    """EqualizedLinear on [Cin, B] -> [Cout, B] (a 1x1 conv at H = W = 1).  ``out`` (no autograd
+    only): a contiguous [Cout, B] destination, e.g. one slice of a stacked buffer."""
     cin, B = x.shape
     cout = w.shape[0]
     geo = linear_geo(B, cin, cout)
+    if out is not None:
+        if torch.is_grad_enabled():
+            raise _lib.GanAmdError("linear(out=...) is a no-grad form")
+        _conv_fwd(geo, _c(x), w.reshape(cout, cin, 1, 1), bias, None, None, alpha, out=out)
+        return out
     return ConvFwd.apply(x.reshape(cin, B, 1, 1), w.reshape(cout, cin, 1, 1), bias, geo, alpha).reshape(cout, B)
 
 

@@ -171,7 +171,9 @@ def test_modconv(ops, B, cin, cout, H, k):
 
 
 @pytest.mark.parametrize("shape,act", [((5, 4, 8, 8), True), ((300, 64), True), ((3, 64, 64, 64), False),
-                                       ((48, 8, 64, 64), True)])
+                                       ((48, 8, 64, 64), True),
+                                       # one block per row (512 < L <= 8192): 5x5 pools, the boundary, ragged
+                                       ((48, 64, 5, 5), True), ((7, 128, 8, 8), False), ((6, 3, 17, 11), True)])
 def test_bn_act(ops, shape, act):
     g = torch.Generator().manual_seed(len(shape) + shape[0])
     C = shape[0]
