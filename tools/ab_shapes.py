@@ -24,6 +24,15 @@ SHAPES_WGRAD = [
     ("fwd", 64, 108, 64, 3, 5, 1, 2, False, 12),
     ("dgrad", 64, 48, 64, 48, 5, 1, 2, True, 20),
 ]
+SHAPES_DG = [   # fwd vs dgrad vs wgrad of the same critic convs (AB_SET=dg)
+    ("fwd", 128, 64, 64, 64, 3, 1, 1, False, 25),
+    ("dgrad", 128, 64, 64, 64, 3, 1, 1, False, 25),
+    ("wgrad", 128, 64, 64, 64, 3, 1, 1, False, 25),
+    ("fwd", 128, 128, 32, 128, 3, 1, 1, False, 25),
+    ("dgrad", 128, 128, 32, 128, 3, 1, 1, False, 25),
+    ("fwd", 64, 256, 16, 256, 3, 1, 1, False, 55),
+    ("dgrad", 64, 256, 16, 256, 3, 1, 1, False, 55),
+]
 SHAPES = [  # (op, B, cin, H, cout, k, stride, pad, scaled, weight = launches per iteration)
     ("fwd", 64, 96, 64, 96, 5, 1, 2, True, 60),
     ("fwd", 64, 48, 64, 48, 5, 1, 2, True, 120),
@@ -47,7 +56,7 @@ def child():
     from gan_amd import ops
     dev = torch.device("cuda")
     tot_t = tot_f = 0.0
-    for op, B, cin, H, cout, k, s, p, scaled, n in (SHAPES_WGRAD if _os.environ.get("AB_SET") == "wgrad" else SHAPES):
+    for op, B, cin, H, cout, k, s, p, scaled, n in {"wgrad": SHAPES_WGRAD, "dg": SHAPES_DG}.get(_os.environ.get("AB_SET"), SHAPES):
         g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
         x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
         y = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
