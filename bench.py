@@ -359,8 +359,9 @@ def main():
     if args.mode == "graph":
         # one HIP graph per distinct phase (synthetic real batch, z, noise and eps are drawn
         # inside; the device Philox stream offsets -- DeviceRNG's, and torch's for the real
-        # batch -- advance on every replay).  N = 1: backward + optimizer in one graph.  N > 1: the RCCL all-reduce of the flat gradient runs eagerly between a
-        # backward graph and an optimizer graph (collectives are kept out of capture).
+        # batch -- advance on every replay).  N = 1: backward + optimizer in one graph.  N > 1:
+        # the RCCL all-reduce of the flat gradient runs eagerly between a backward graph and an
+        # optimizer graph (collectives are kept out of capture).
         # All phase graphs share ONE memory pool: the phases replay strictly one after another,
         # so a later graph may reuse what an earlier one freed (per-graph pools would hold every
         # phase's peak at once: > 250 GiB for the lazy config at B = 128).
