@@ -75,6 +75,8 @@ _SIGS = {
     "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),
     "ganamd_prelu_bwd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_long, vp, vp, vp, vp, vp]),
     "ganamd_resample2d": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int, vp]),
+    "ganamd_resample2d_sum": (c_int, [vp, vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int,
+                                      vp]),
     "ganamd_plane_dot": (c_int, [vp, vp, c_long, c_long, c_float, vp, vp]),
     "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, c_int, vp, vp]),
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),

@@ -701,8 +701,9 @@ __global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int
 inline __host__ __device__ int align4(int n) { return (n + 3) & ~3; }
 
 template <int V>
-__global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict__ x, long planes, int IH, int IW,
-                                                         float* __restrict__ y, int OH, int OW,
+__global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict__ x, const float* __restrict__ x2,
+                                                         long planes, int IH, int IW, float* __restrict__ y, int OH,
+                                                         int OW,
                                                          const int32_t* __restrict__ ri, const float* __restrict__ rw,
                                                          int KR, const int32_t* __restrict__ ci,
                                                          const float* __restrict__ cw, int KC, int ppb) {
@@ -719,11 +720,15 @@ __global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict
   const int tid = threadIdx.x;
   const int nin = np * IH * IW;
   const float* xg = x + p0 * IH * IW;
-  if (((IH * IW) & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-    for (int i = tid; i < nin / 4; i += kNT)
-      reinterpret_cast<f4*>(xs)[i] = reinterpret_cast<const f4*>(xg)[i];
+  const float* x2g = x2 ? x2 + p0 * IH * IW : nullptr;   // resample of a sum: summed while staging
+  if (((IH * IW) & 3) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(x2)) & 15) == 0) {
+    for (int i = tid; i < nin / 4; i += kNT) {
+      f4 t = reinterpret_cast<const f4*>(xg)[i];
+      if (x2g) t += reinterpret_cast<const f4*>(x2g)[i];
+      reinterpret_cast<f4*>(xs)[i] = t;
+    }
   } else {
-    for (int i = tid; i < nin; i += kNT) xs[i] = xg[i];
+    for (int i = tid; i < nin; i += kNT) xs[i] = x2g ? xg[i] + x2g[i] : xg[i];
   }
   for (int i = tid; i < OW * KC; i += kNT) {
     cws[i] = cw[i];
@@ -932,6 +937,12 @@ int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const
 
 int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
                       const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t st) {
+  return ganamd_resample2d_sum(x, nullptr, planes, IH, IW, y, OH, OW, ri, rw, KR, ci, cw, KC, st);
+}
+
+int ganamd_resample2d_sum(const float* x, const float* x2, long planes, int IH, int IW, float* y, int OH, int OW,
+                          const int32_t* ri, const float* rw, int KR, const int32_t* ci, const float* cw, int KC,
+                          hipStream_t st) {
   if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;
   // planes per workgroup: ~2K staged inputs but <= ~8K outputs (an upsampling adjoint such as
   // pool5's 5x5 -> 64x64 would otherwise pack 81 planes, 330K outputs, into each of a few dozen
@@ -946,11 +957,11 @@ int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int
   const long blocks = (planes + ppb - 1) / ppb;
   const size_t bytes = 4 * (size_t)(align4(ppb * IH * IW) + align4(ppb * IH * OW) + 2 * (OW * KC + OH * KR));
   if (V == 4)
-    hipLaunchKernelGGL(resample2d_kernel<4>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, planes, IH, IW, y, OH,
-                       OW, ri, rw, KR, ci, cw, KC, ppb);
+    hipLaunchKernelGGL(resample2d_kernel<4>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, x2, planes, IH, IW, y,
+                       OH, OW, ri, rw, KR, ci, cw, KC, ppb);
   else
-    hipLaunchKernelGGL(resample2d_kernel<1>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, planes, IH, IW, y, OH,
-                       OW, ri, rw, KR, ci, cw, KC, ppb);
+    hipLaunchKernelGGL(resample2d_kernel<1>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, x2, planes, IH, IW, y,
+                       OH, OW, ri, rw, KR, ci, cw, KC, ppb);
   return ok(hipGetLastError());
 }
 

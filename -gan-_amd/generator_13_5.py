@@ -116,11 +116,15 @@ class SKAttention_conv(nn.Module):
                                                       nn.PReLU(planes), EqualizedLinear(planes, planes)))
 
     def forward(self, feas):
-        u = feas[0]
-        for f in feas[1:]:
-            u = u + f
-        assert u.shape[2] >= 8
-        t = ops.resample(u, "pool5")
+        if len(feas) == 2 and not torch.is_grad_enabled():   # pool of the branch sum, the sum never stored
+            assert feas[0].shape[2] >= 8
+            t = ops.resample_sum(feas[0], feas[1], "pool5")
+        else:
+            u = feas[0]
+            for f in feas[1:]:
+                u = u + f
+            assert u.shape[2] >= 8
+            t = ops.resample(u, "pool5")
         cm = self.conv_main
         t = _conv_bn_act(cm[0], cm[1], cm[2], t)
         t = _conv_bn_act(cm[3], cm[4], cm[5], t)

@@ -737,6 +737,25 @@ def resample(x, kind: str):
     return Resample.apply(x, tables.table(kind, x.shape[2], x.device), False)
 
 
+def resample_sum(x1, x2, kind: str):
+    """``resample(x1 + x2, kind)`` without materialising the sum (no autograd: the sum is formed
+    while the kernel stages its input planes, ganamd_resample2d_sum)."""
+    if torch.is_grad_enabled():
+        raise _lib.GanAmdError("resample_sum is a no-grad form")
+    x1, x2 = _c(x1), _c(x2)
+    if x1.shape != x2.shape:
+        raise _lib.GanAmdError(f"resample_sum: {tuple(x1.shape)} vs {tuple(x2.shape)}")
+    t = tables.table(kind, x1.shape[2], x1.device)
+    idx, w, k = t.fwd
+    C, B, n_in = x1.shape[0], x1.shape[1], t.n_in
+    if x1.dim() != 4 or x1.shape[2] != n_in or x1.shape[3] != n_in:
+        raise _lib.GanAmdError(f"resample_sum: input {tuple(x1.shape)} vs table {n_in}->{t.n_out}")
+    y = torch.empty((C, B, t.n_out, t.n_out), device=x1.device, dtype=torch.float32)
+    check(LIB.ganamd_resample2d_sum(ptr(x1), ptr(x2), C * B, n_in, n_in, ptr(y), t.n_out, t.n_out, iptr(idx), ptr(w),
+                                    k, iptr(idx), ptr(w), k, stream()), "resample2d_sum")
+    return y
+
+
 # ------------------------------------------------------------------------------------------
 # per-plane mean (AdaptiveAvgPool2d(1)) -> [C, B]
 # ------------------------------------------------------------------------------------------

@@ -180,6 +180,11 @@ int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const
  * ------------------------------------------------------------------------------------- */
 int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
                       const float* rw, int KR, const int32_t* ci, const float* cw, int KC, hipStream_t stream);
+/* The same resampling of (x + x2) (the sum formed while staging; SK attention's pool of the branch
+ * sum u = sum_m feas_m, generator_13_5.py:82-84, without materialising u). */
+int ganamd_resample2d_sum(const float* x, const float* x2, long planes, int IH, int IW, float* y, int OH, int OW,
+                          const int32_t* ri, const float* rw, int KR, const int32_t* ci, const float* cw, int KC,
+                          hipStream_t stream);
 
 /* out[p] = scale * sum_{hw} a[p][hw] * (b ? b[p][hw] : 1)   (planes of HW elements).
  * Replaces AdaptiveAvgPool2d(1) (generator_13_5.py:52,362) and the per-(channel,sample)

@@ -623,3 +623,16 @@ def test_linear_bn_act_fused(ops, B, cin, cout, act):
     assert rel(y.t(), ref) < 1e-5
     assert rel(bn_g.running_mean, bn.running_mean) < 1e-5
     assert rel(bn_g.running_var, bn.running_var) < 1e-5
+
+
+@pytest.mark.parametrize("kind,C,B,n", [("pool5", 48, 8, 64), ("pool5", 96, 3, 32), ("smooth", 7, 5, 32)])
+def test_resample_sum(ops, kind, C, B, n):
+    """ganamd_resample2d_sum (no-grad SK-attention pool of the branch sum) == resample of the
+    materialised sum, bit for bit (the same fp32 sum, formed while staging)."""
+    g = torch.Generator().manual_seed(C + B + n)
+    a = torch.randn(C, B, n, n, generator=g).to(DEV)
+    b = torch.randn(C, B, n, n, generator=g).to(DEV)
+    with torch.no_grad():
+        ref = ops.resample(a + b, kind)
+        got = ops.resample_sum(a, b, kind)
+    assert torch.equal(got, ref)
