@@ -77,6 +77,7 @@ _SIGS = {
     "ganamd_resample2d": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int, vp]),
     "ganamd_resample2d_sum": (c_int, [vp, vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int,
                                       vp]),
+    "ganamd_plane_dot_pair": (c_int, [vp, vp, vp, c_long, c_long, vp, vp, vp]),
     "ganamd_plane_dot": (c_int, [vp, vp, c_long, c_long, c_float, vp, vp]),
     "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, c_int, vp, vp]),
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),

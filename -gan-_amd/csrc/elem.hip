@@ -682,6 +682,31 @@ __global__ __launch_bounds__(kNT) void plane_dot_big_kernel(const float* __restr
   if (threadIdx.x == 0) out[p] = scale * acc;
 }
 
+// Two plane dots sharing a: out1[p] = sum a*b1, out2[p] = sum a*b2 -- the modulated conv's
+// backward needs <gy, y> and <gy, noise> per (channel, sample); one pass reads gy once.
+__global__ __launch_bounds__(kNT) void plane_dot_pair_kernel(const float* __restrict__ a, const float* __restrict__ b1,
+                                                             const float* __restrict__ b2, long HW,
+                                                             float* __restrict__ out1, float* __restrict__ out2) {
+  __shared__ float sh[4];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const long p = blockIdx.x;
+  const f4* a4 = reinterpret_cast<const f4*>(a + p * HW);
+  const f4* c4 = reinterpret_cast<const f4*>(b1 + p * HW);
+  const f4* d4 = reinterpret_cast<const f4*>(b2 + p * HW);
+  float s1 = 0.f, s2 = 0.f;
+  for (long i = threadIdx.x; i < HW / 4; i += kNT) {
+    const f4 u = a4[i], v = c4[i], w = d4[i];
+    s1 += u[0] * v[0] + u[1] * v[1] + u[2] * v[2] + u[3] * v[3];
+    s2 += u[0] * w[0] + u[1] * w[1] + u[2] * w[2] + u[3] * w[3];
+  }
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
+  if (threadIdx.x == 0) {
+    out1[p] = s1;
+    out2[p] = s2;
+  }
+}
+
 __global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int T, float* __restrict__ out) {
   for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < rows; r += (long)gridDim.x * blockDim.x) {
     const float* p = w + r * T;
@@ -976,6 +1001,15 @@ int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float
     return ok(hipGetLastError());
   }
   hipLaunchKernelGGL(plane_dot_kernel, dim3(blocks), dim3(kNT), 0, st, a, b, planes, HW, scale, out);
+  return ok(hipGetLastError());
+}
+
+int ganamd_plane_dot_pair(const float* a, const float* b1, const float* b2, long planes, long HW, float* out1,
+                          float* out2, hipStream_t st) {
+  if (!a || !b1 || !b2 || !out1 || !out2 || planes <= 0 || HW <= 0 || HW % 4 ||
+      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b1) | reinterpret_cast<uintptr_t>(b2)) & 15))
+    return GANAMD_EINVAL;
+  hipLaunchKernelGGL(plane_dot_pair_kernel, dim3((unsigned)planes), dim3(kNT), 0, st, a, b1, b2, HW, out1, out2);
   return ok(hipGetLastError());
 }
 

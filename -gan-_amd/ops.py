@@ -791,6 +791,20 @@ def plane_dot(a, b, scale=1.0):
     return out
 
 
+def plane_dot_pair(a, b1, b2):
+    """(<a, b1>, <a, b2>) per plane in one pass over a (ganamd_plane_dot_pair), or None when the
+    planes do not suit its 16-byte loads (the caller then takes two plane_dot launches)."""
+    a, b1, b2 = _c(a), _c(b1), _c(b2)
+    C, B, H, W = a.shape
+    if (H * W) % 4 or any(t.data_ptr() % 16 for t in (a, b1, b2)):
+        return None
+    o1 = torch.empty((C, B), device=a.device, dtype=torch.float32)
+    o2 = torch.empty_like(o1)
+    check(LIB.ganamd_plane_dot_pair(ptr(a), ptr(b1), ptr(b2), C * B, H * W, ptr(o1), ptr(o2), stream()),
+          "plane_dot_pair")
+    return o1, o2
+
+
 # ------------------------------------------------------------------------------------------
 # weight-modulated conv (StyleGAN2 demodulation) -- generator only
 # ------------------------------------------------------------------------------------------
@@ -828,11 +842,15 @@ class ModConv(Function):
             (x, s, d, w, y), ns, noise = ctx.saved_tensors, None, None
         geo, c = ctx.geo, ctx.c
         gns = None
-        pdn = None
-        if noise is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[6]):
+        pdn = pdy = None
+        if noise is not None and ctx.needs_input_grad[2]:
+            pair = plane_dot_pair(gy, y, noise)             # <gy, y> and <gy, noise> in one pass
+            if pair is not None:
+                pdy, pdn = pair
+        if noise is not None and pdn is None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[6]):
             pdn = plane_dot(gy, noise)                      # [C, B]: sum_hw gy * noise
-            if ctx.needs_input_grad[6]:
-                gns = pdn.sum(1)
+        if pdn is not None and ctx.needs_input_grad[6]:
+            gns = pdn.sum(1)
         gy = _c(gy)
         gx = gs = gd = gw = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
@@ -844,7 +862,8 @@ class ModConv(Function):
             check(LIB.ganamd_mix_bwd(1, ptr(x), None, None, None, ptr(s), P, HW, ptr(gxs), ptr(gx), None, None, None,
                                      ptr(gs), stream()), "mix_bwd")
         if ctx.needs_input_grad[2]:
-            pdy = plane_dot(gy, y)                          # y = d * conv (+ ns * noise)
+            if pdy is None:
+                pdy = plane_dot(gy, y)                      # y = d * conv (+ ns * noise)
             if pdn is not None:
                 pdy = pdy - ns[:, None] * pdn
             gd = pdy / d                                    # dL/dd = sum gy * conv

@@ -191,6 +191,10 @@ int ganamd_resample2d_sum(const float* x, const float* x2, long planes, int IH, 
  * reductions of the modulated-conv / SK / SE backward. */
 int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float scale, float* out,
                      hipStream_t stream);
+/* out1[p] = sum_hw a*b1, out2[p] = sum_hw a*b2 in one pass over a (HW % 4 == 0, 16-byte aligned
+ * planes): the modulated conv backward's <gy, y> and <gy, noise> (generator_13_5.py:234-248, 265). */
+int ganamd_plane_dot_pair(const float* a, const float* b1, const float* b2, long planes, long HW, float* out1,
+                          float* out2, hipStream_t stream);
 
 /* out[c] (=|+= with accumulate) sum_{l} a[c][l] * (b ? b[c][l] : 1) over rows of length L
  * (with b = NULL and accumulate = 1: a conv bias gradient added into the flat gradient buffer). */

@@ -636,3 +636,15 @@ def test_resample_sum(ops, kind, C, B, n):
         ref = ops.resample(a + b, kind)
         got = ops.resample_sum(a, b, kind)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("C,B,H", [(48, 8, 64), (96, 4, 16), (7, 3, 2)])
+def test_plane_dot_pair(ops, C, B, H):
+    """ganamd_plane_dot_pair: <a, b1> and <a, b2> per plane in one pass, against float64."""
+    g = torch.Generator().manual_seed(C * B + H)
+    a, b1, b2 = (torch.randn(C, B, H, H, generator=g, dtype=torch.float64) for _ in range(3))
+    with torch.no_grad():
+        out = ops.plane_dot_pair(a.float().to(DEV), b1.float().to(DEV), b2.float().to(DEV))
+    assert out is not None
+    assert rel(out[0], (a * b1).sum((2, 3))) < 1e-5
+    assert rel(out[1], (a * b2).sum((2, 3))) < 1e-5
