@@ -1564,10 +1564,12 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(
     float v[V];
     if constexpr (VEC) {
       f32x4 a = *reinterpret_cast<const f32x4*>(slab + e);
+#pragma unroll 8   // the slab loads of 8 splits in flight at once (same summation order)
       for (int s = 1; s < S; ++s) a += *reinterpret_cast<const f32x4*>(slab + (long)s * total + e);
       v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
     } else {
       float a = slab[e];
+#pragma unroll 8   // the slab loads of 8 splits in flight at once (same summation order)
       for (int s = 1; s < S; ++s) a += slab[(long)s * total + e];
       v[0] = a;
     }
@@ -1617,11 +1619,13 @@ __global__ __launch_bounds__(256) void wgrad_split_reduce_kernel(const float* __
     const unsigned e = u * V;
     if constexpr (VEC) {
       f32x4 a = *reinterpret_cast<const f32x4*>(slab + e);
+#pragma unroll 8   // the slab loads of 8 splits in flight at once (same summation order)
       for (int s = 1; s < S; ++s) a += *reinterpret_cast<const f32x4*>(slab + (long)s * total + e);
       if (accumulate) a += *reinterpret_cast<const f32x4*>(out + e);
       *reinterpret_cast<f32x4*>(out + e) = a;
     } else {
       float a = slab[e];
+#pragma unroll 8   // the slab loads of 8 splits in flight at once (same summation order)
       for (int s = 1; s < S; ++s) a += slab[(long)s * total + e];
       out[e] = accumulate ? out[e] + a : a;
     }
@@ -1797,7 +1801,22 @@ __global__ __launch_bounds__(64 * NW) void linear_gemm_kernel(ConvArgs p, BNArgs
     // with the batch mean / biased variance of the row; running stats take the unbiased variance
     static_assert(LBN == 64 && LBM % NW == 0, "BN epilogue: one wave per 64-column row");
     const float inv_n = 1.f / (float)N;
-    for (int row = wave; row < LBM; row += NW) {
+    constexpr int RW = LBM / NW;                   // rows per wave
+    // the rows' constants are fetched together up front (one memory round trip, not one per row)
+    float cb[RW], cg[RW], cbt[RW], ca[RW], rm[RW], rv[RW];
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int m = min(m0 + wave + NW * q, p.M - 1);
+      rm[q] = bn.running_mean[m];
+      rv[q] = bn.running_var[m];
+      cb[q] = p.bias ? p.bias[m] : 0.f;
+      cg[q] = bn.gamma[m];
+      cbt[q] = bn.beta[m];
+      ca[q] = p.act ? p.act[m] : 1.f;
+    }
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int row = wave + NW * q;
       const int m = m0 + row;
       if (m >= p.M) break;                         // wave-uniform
       const bool ok = lane < N;
@@ -1805,36 +1824,45 @@ __global__ __launch_bounds__(64 * NW) void linear_gemm_kernel(ConvArgs p, BNArgs
       if (ok) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) v += red[w][row * LBN + lane];
-        v *= p.alpha;
-        if (p.bias) v += p.bias[m];
+        v = v * p.alpha + cb[q];
       }
       const float mean = wave_sum(v) * inv_n;
       const float d = ok ? v - mean : 0.f;
       const float var = wave_sum(d * d) * inv_n;
-      float yv = d * (1.f / sqrtf(var + bn.eps)) * bn.gamma[m] + bn.beta[m];
-      if (p.act) yv = yv > 0.f ? yv : p.act[m] * yv;
+      float yv = d * (1.f / sqrtf(var + bn.eps)) * cg[q] + cbt[q];
+      yv = yv > 0.f ? yv : ca[q] * yv;
       if (ok) p.y[(long)m * p.ldy + lane] = yv;
       if (lane == 0) {
         const float mo = bn.momentum;
-        bn.running_mean[m] = (1.f - mo) * bn.running_mean[m] + mo * mean;
-        bn.running_var[m] = (1.f - mo) * bn.running_var[m] + mo * var * ((float)N / (float)(N - 1));
+        bn.running_mean[m] = (1.f - mo) * rm[q] + mo * mean;
+        bn.running_var[m] = (1.f - mo) * rv[q] + mo * var * ((float)N / (float)(N - 1));
       }
     }
     return;
   }
-  for (int idx = tid; idx < LBM * LBN; idx += 64 * NW) {
-    const int row = idx / LBN, col = idx - row * LBN;
-    const int m = m0 + row, n = n0 + col;
-    if (m >= p.M || n >= N) continue;
+  // each thread owns EI elements (rows tid / LBN + q * (64 NW / LBN), one column); their per-row
+  // constants are loaded together (clamped indices, no per-element branches) before the stores
+  constexpr int EI = LBM * LBN / (64 * NW);
+  const int col = tid % LBN, n = n0 + col, nc = min(n, N - 1);
+  float osc[EI], cb[EI], cn[EI], ca[EI];
+#pragma unroll
+  for (int q = 0; q < EI; ++q) {
+    const int m = min(m0 + (tid + q * 64 * NW) / LBN, p.M - 1);
+    osc[q] = p.oscale ? p.oscale[m * p.g.B + nc / p.ohw] : 1.f;
+    cb[q] = p.bias ? p.bias[m] : 0.f;
+    cn[q] = p.noise ? p.noise_scale[m] * p.noise[(long)m * p.ldy + nc] : 0.f;
+    ca[q] = p.act ? p.act[m] : 1.f;
+  }
+#pragma unroll
+  for (int q = 0; q < EI; ++q) {
+    const int idx = tid + q * 64 * NW;
+    const int m = m0 + idx / LBN;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][idx];
-    v *= p.alpha;
-    if (p.oscale) v *= p.oscale[m * p.g.B + n / p.ohw];
-    if (p.bias) v += p.bias[m];
-    if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + n];
-    if (p.act) v = v > 0.f ? v : p.act[m] * v;
-    p.y[(long)m * p.ldy + n] = v;
+    v = (v * p.alpha) * osc[q] + cb[q] + cn[q];
+    v = v > 0.f ? v : ca[q] * v;
+    if (m < p.M && n < N) p.y[(long)m * p.ldy + n] = v;
   }
 }
 
