@@ -103,6 +103,8 @@ _SIGS = {
                                      vp, vp, vp]),
     "ganamd_philox_uniform": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_normal": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
+    "ganamd_philox_draw": (c_int, [vp, c_long, ctypes.c_uint64, vp, ctypes.c_uint32, c_int, c_int, vp]),
+    "ganamd_philox_advance": (c_int, [vp, vp]),
     "ganamd_image_batch_workspace": (c_size_t, [c_int, c_int, c_int]),
     "ganamd_image_batch": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, c_int, c_int, vp, vp, c_int, c_int, vp, vp,
                                    vp, vp, vp]),

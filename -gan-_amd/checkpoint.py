@@ -51,10 +51,12 @@ class CheckpointMixin:
                  "method": train_name, "epoch": e, "i": ii,
                  "optimizer_G": self.optimizer_G.state_dict(), "optimizer_D": self.optimizer_D.state_dict()}
         path = ckpt_path(self.ckpt_root, self.generator_name, self.discriminator_name, train_name, e, ii)
-        if _is_dist() and torch.distributed.get_rank() != 0:
-            return path          # data parallel: the replicas are identical, rank 0 writes the file
-        os.makedirs(self.ckpt_root, exist_ok=True)
-        torch.save(state, path)
+        if not _is_dist() or torch.distributed.get_rank() == 0:
+            # data parallel: the replicas are identical, rank 0 writes the file
+            os.makedirs(self.ckpt_root, exist_ok=True)
+            torch.save(state, path)
+        if _is_dist():
+            torch.distributed.barrier()     # no rank returns the path before the file is complete
         return path
 
     def _load(self, name):

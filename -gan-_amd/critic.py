@@ -606,7 +606,9 @@ class _CriticGrad(Function):
     @staticmethod
     def forward(ctx, seed, run, first_order_params, *params):
         ctx.run, ctx.params = run, params
-        return run.backward(seed, params=first_order_params, need_input=True)
+        gx = run.backward(seed, params=first_order_params, need_input=True)
+        run.G.pop(0, None)     # the run must not hold this node's output (ctx -> run -> output cycle)
+        return gx
 
     @staticmethod
     @torch.autograd.function.once_differentiable

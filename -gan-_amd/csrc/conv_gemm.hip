@@ -1293,14 +1293,8 @@ int num_cus();
 double list_makespan(long F, double L, long R, double d, long slots);
 
 // Price of the extra reduce launch of a split GEMM (its own ~5 us run time on tiny data plus the
-// dependent-launch boundary); GANAMD_REDUCE_US overrides it (tuning experiments).
-double reduce_launch_us() {
-  static const double v = [] {
-    const char* e = getenv("GANAMD_REDUCE_US");
-    return e ? atof(e) : 3.0;
-  }();
-  return v;
-}
+// dependent-launch boundary).
+constexpr double reduce_launch_us() { return 3.0; }
 
 // wgrad split-K by a small cost model: a GEMM of `tiles` output tiles, each `kt_total` K-steps of
 // `kflop` FLOPs, runs in ceil(tiles*s / slots) rounds of blocks (slots = resident blocks per CU

@@ -7,6 +7,13 @@
 //            z0 = r cos(2 pi u2), z1 = r sin(2 pi u2), u2 = (w1 >> 8) * 2^-24
 // The stream offset lives in device memory and is advanced by one per call (a one-thread launch
 // after the draw), so a captured graph draws fresh numbers on every replay.
+//
+// Concurrent consumers never share a counter:
+//   * each consumer owns its offset word (rng.py DeviceRNG.fork gives stream s the offsets
+//     s * 2^40 + k), and only the stream that owns a word ever advances it;
+//   * draws that run concurrently on ONE offset (a generator forward's per-draw noise inside
+//     parallel branch streams) read it without advancing and put a distinct draw index `sub` into
+//     counter word 1 (group index < 2^32 there); the owner advances once after joining them.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -41,11 +48,11 @@ __device__ __forceinline__ void philox10(uint32_t (&c)[4], uint64_t seed) {
 
 template <bool NORMAL>
 __global__ __launch_bounds__(kNT) void philox_kernel(float* __restrict__ out, long n, uint64_t seed,
-                                                     const uint64_t* __restrict__ offset) {
+                                                     const uint64_t* __restrict__ offset, uint32_t sub) {
   const uint64_t off = *offset;
   const long groups = (n + 3) / 4;
   for (long g = blockIdx.x * (long)kNT + threadIdx.x; g < groups; g += (long)gridDim.x * kNT) {
-    uint32_t c[4] = {(uint32_t)g, (uint32_t)((uint64_t)g >> 32), (uint32_t)off, (uint32_t)(off >> 32)};
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)((uint64_t)g >> 32) + sub, (uint32_t)off, (uint32_t)(off >> 32)};
     philox10(c, seed);
     float v[4];
     if (NORMAL) {
@@ -73,15 +80,17 @@ __global__ __launch_bounds__(kNT) void philox_kernel(float* __restrict__ out, lo
 
 __global__ void offset_advance_kernel(uint64_t* offset) { *offset += 1; }
 
-int launch(bool normal, float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t st) {
+int launch(bool normal, float* out, long n, uint64_t seed, uint64_t* offset, uint32_t sub, bool advance,
+           hipStream_t st) {
   if (!out || !offset || n <= 0) return GANAMD_EINVAL;
   const long groups = (n + 3) / 4;
+  if (sub != 0 && groups > (1L << 32)) return GANAMD_EINVAL;    // word 1 must hold the index alone
   const unsigned blocks = (unsigned)std::min<long>((groups + kNT - 1) / kNT, 2048L * 8);
   if (normal)
-    hipLaunchKernelGGL(philox_kernel<true>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, offset);
+    hipLaunchKernelGGL(philox_kernel<true>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, offset, sub);
   else
-    hipLaunchKernelGGL(philox_kernel<false>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, offset);
-  hipLaunchKernelGGL(offset_advance_kernel, dim3(1), dim3(1), 0, st, offset);
+    hipLaunchKernelGGL(philox_kernel<false>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, offset, sub);
+  if (advance) hipLaunchKernelGGL(offset_advance_kernel, dim3(1), dim3(1), 0, st, offset);
   return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
@@ -90,11 +99,22 @@ int launch(bool normal, float* out, long n, uint64_t seed, uint64_t* offset, hip
 extern "C" {
 
 int ganamd_philox_uniform(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream) {
-  return launch(false, out, n, seed, offset, stream);
+  return launch(false, out, n, seed, offset, 0, true, stream);
 }
 
 int ganamd_philox_normal(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream) {
-  return launch(true, out, n, seed, offset, stream);
+  return launch(true, out, n, seed, offset, 0, true, stream);
+}
+
+int ganamd_philox_draw(float* out, long n, uint64_t seed, uint64_t* offset, uint32_t sub, int normal, int advance,
+                       hipStream_t stream) {
+  return launch(normal != 0, out, n, seed, offset, sub, advance != 0, stream);
+}
+
+int ganamd_philox_advance(uint64_t* offset, hipStream_t stream) {
+  if (!offset) return GANAMD_EINVAL;
+  hipLaunchKernelGGL(offset_advance_kernel, dim3(1), dim3(1), 0, stream, offset);
+  return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
 
 }  // extern "C"

@@ -209,7 +209,15 @@ class Discriminator(nn.Module):
 
         Runs the critic as the explicit layer program of critic.py: one autograd node whose
         backward (and, under create_graph, double backward) are kernel sweeps over the saved
-        activations -- no per-layer autograd graph."""
+        activations -- no per-layer autograd graph.
+
+        Parameter gradients: the sweeps accumulate them straight into each parameter's ``.grad``
+        (the optimizer's flat gradient buffer) and hand autograd None for the parameters, which
+        is what ``loss.backward()`` -- the only way train/wgangp.py:20-71 uses them -- needs.  A
+        consequence: ``torch.autograd.grad(loss, D.parameters())`` finds no gradient (it raises
+        "appears to not have been used in the graph", or returns None with allow_unused=True;
+        the result is ALSO added to ``.grad``), and hooks registered on D's parameters do not
+        fire.  Use ``forward_autograd`` for per-parameter autograd semantics."""
         return critic.critic_forward(self, input, segments)
 
     def forward_autograd(self, input, segments: int = 1):

@@ -202,8 +202,6 @@ class SKConv(nn.Module):
         self.sk_attention = (SKAttention_conv if image_size > 4 else SKAttention_fc)(out_planes, m)
 
     def forward(self, x):
-        # (the k3 / k5 branches inside one of ResnetInit's parallel StyleBlocks would nest stream
-        # forks; nested forks crash HIP graph capture here, so only ResnetInit branches)
         feas = [_conv_bn_act(getattr(self, f"conv_{i}"), getattr(self, f"BatchNorm_{i}"),
                              getattr(self, f"nonlinear_{i}"), x) for i in range(self.M)]
         return _mix(feas, self.sk_attention(feas))
@@ -281,13 +279,6 @@ class StyleConv(nn.Module):
         return self.conv(x, w, noise, self.scale_noise if self.use_noise else None, act)
 
 
-import os as _os
-
-# stream-branch placement (A/B): ResnetInit's four StyleBlocks (default) or the SK k3/k5 branches
-RESNET_BRANCHES = [_os.environ.get("GANAMD_RESNET_BRANCHES", "1") != "0"]
-SK_BRANCHES = [_os.environ.get("GANAMD_SK_BRANCHES", "0") != "0"]
-
-
 class SKStyleConv(nn.Module):
     """k3 || k5 StyleConv + noise + PReLU, SK-mixed (generator_13_5.py:269-295)."""
 
@@ -302,14 +293,9 @@ class SKStyleConv(nn.Module):
         self.sk_attention = (SKAttention_conv if image_size > 4 else SKAttention_fc)(out_planes, m)
 
     def forward(self, x, w):
-        if SK_BRANCHES[0]:
-            feas = [None] * self.M
-            with ops.Branches(x.device, self.M) as br:      # the k3 / k5 branches are independent
-                for i in range(self.M):
-                    with br[i]:
-                        feas[i] = getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight)
-        else:
-            feas = [getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
+        # the k3 / k5 branches run in order on the current stream: the stream-level parallelism
+        # is ResnetInit's four StyleBlocks (ops.Branches does not nest)
+        feas = [getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
         return _mix(feas, self.sk_attention(feas))
 
 
@@ -355,11 +341,6 @@ class ResnetInit(nn.Module):
 
     def forward(self, x, w):
         x_res, x_tr = x
-        if not RESNET_BRANCHES[0]:
-            r_r, r_t = self.residual(x_res, w), self.residual_across(x_res, w)
-            t_t, t_r = self.transient(x_tr, w), self.transient_across(x_tr, w)
-            return (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
-                    ops.add_prelu(r_t, t_t, self.activation_transient.weight))
         # the four StyleBlocks are independent: on a GPU each runs on its own HIP stream (their
         # hundreds of small, launch-bound kernels overlap; a captured graph keeps the branches),
         # issued in the reference's order so the noise draws keep theirs
@@ -594,18 +575,31 @@ class _NoiseHub:
     (DeviceRNG.noise_bulk) and a previous forward at the same batch recorded the draw shapes,
     the hub draws ALL of a forward's noise with one launch at its start and hands out views in
     the same order (one launch instead of 253; inside a captured graph the bulk draw is captured
-    too, so every replay gets fresh noise).  A replaying source (ReplayRNG) keeps the per-draw
-    path and the reference's draw order."""
+    too, so every replay gets fresh noise).  Otherwise, with an indexed source
+    (DeviceRNG.noise_at), draw i of the forward reads the generator's offset without advancing it
+    and carries i in its counter, and the forward advances the offset once at its end: the draws
+    made inside ResnetInit's parallel branch streams never race on the offset word.  A replaying
+    source (ReplayRNG) keeps the per-draw path and the reference's draw order."""
 
     def __init__(self):
-        self.source = None
+        self.source = None          # shape -> tensor: per-draw, advancing (ReplayRNG.noise)
         self.bulk_source = None     # numel -> flat N(0,1) tensor, or None (per-draw only)
+        self.indexed_source = None  # (shape, i >= 1) -> tensor at the current offset, no advance
+        self.advance = None         # advances the indexed source's offset (end of the forward)
         self.shapes = {}            # batch -> the draw shapes of one forward
         self._rec = None
         self._bulk = None
+        self._idx = 0
+
+    def attach(self, rng):
+        """Draw from ``rng`` (DeviceRNG: bulk / indexed; ReplayRNG: per draw in call order)."""
+        self.source = rng.noise
+        self.bulk_source = getattr(rng, "noise_bulk", None)
+        self.indexed_source = getattr(rng, "noise_at", None)
+        self.advance = getattr(rng, "advance", None) if self.indexed_source is not None else None
 
     def begin(self, batch):
-        self._rec, self._bulk = [], None
+        self._rec, self._bulk, self._idx = [], None, 0
         bulk = self.bulk_source if self.source is not None else None
         shapes = self.shapes.get(batch)
         if bulk is not None and shapes:
@@ -615,7 +609,9 @@ class _NoiseHub:
     def end(self, batch):
         if self._rec is not None:
             self.shapes[batch] = self._rec
-        self._rec, self._bulk = None, None
+        if self._idx and self.advance is not None:   # on the forward's stream, after the joins
+            self.advance()
+        self._rec, self._bulk, self._idx = None, None, 0
 
     def noise(self, shape_nchw):
         if self._rec is not None:
@@ -628,6 +624,9 @@ class _NoiseHub:
                 self._bulk = (buf, shapes, i + 1, off + n)
                 return buf[off:off + n].view(C, B, H, W)
             self._bulk = None           # the draw sequence changed: per-draw from here on
+        if self.indexed_source is not None:
+            self._idx += 1
+            return self.indexed_source(shape_nchw, self._idx)
         if self.source is not None:
             return self.source(shape_nchw)
         B, C, H, W = shape_nchw

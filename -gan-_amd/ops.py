@@ -1226,20 +1226,25 @@ _STREAM_POOL: dict = {}
 class Branches:
     """``with Branches(dev, n) as br: with br[i]: ...`` -- each branch body runs on its own pooled
     HIP stream, forked from the current stream on entry and joined back into it on exit (a captured
-    graph gets parallel branches).  Nested branch sets take streams from a pool of their own
-    nesting depth.  Tensors a branch allocates are consumed on the current stream only after the
-    join, and every later branch forks after that consumer, so the caching allocator never hands a
-    branch's memory to work that could overlap its readers.  On the CPU, or with BRANCH_STREAMS[0]
-    False, the bodies run inline."""
+    graph gets parallel branches).  Tensors a branch allocates are consumed on the current stream
+    only after the join, and every later branch forks after that consumer, so the caching allocator
+    never hands a branch's memory to work that could overlap its readers.
+
+    Branch sets do not nest: inside a branch a further set runs inline.  (A nested set would need
+    streams of its own per enclosing branch -- one shared pool per nesting depth, as an earlier
+    build had, makes sibling branches fork and join through the same inner streams, serialising
+    them and letting the allocator recycle one sibling's inner blocks while the other still reads
+    them; the k3/k5 split inside the parallel StyleBlocks also measured slower, 37.9 vs 39.8
+    img/s.)  On the CPU, or with BRANCH_STREAMS[0] False, the bodies run inline."""
 
     _depth = [0]
 
     def __init__(self, device, n):
         dev = torch.device(device)
-        self.on = BRANCH_STREAMS[0] and dev.type == "cuda" and n > 1
+        self.on = BRANCH_STREAMS[0] and dev.type == "cuda" and n > 1 and Branches._depth[0] == 0
         self.n = n
         if self.on:
-            key = (dev.index if dev.index is not None else torch.cuda.current_device(), Branches._depth[0])
+            key = dev.index if dev.index is not None else torch.cuda.current_device()
             pool = _STREAM_POOL.setdefault(key, [])
             while len(pool) < n:
                 pool.append(torch.cuda.Stream(device=dev))

@@ -65,11 +65,22 @@ class Train(CheckpointMixin):
         return (FusedAdamW(self.generator, lr=0.0001, betas=(0.5, 0.999)),
                 FusedAdamW(self.discriminator, lr=0.0004, betas=(0.5, 0.999)))
 
+    @property
+    def rng_g(self):
+        """The generator's z and in-forward noise source: stream 1 of ``rng`` (DeviceRNG.fork), so
+        a fake batch made on a second HIP stream never shares a Philox counter with the critic
+        step's eps draws on the first; ReplayRNG forks to itself (the reference's one sequence)."""
+        r = self.rng
+        c = self.__dict__.get("_rng_g")
+        if c is None or c[0] is not r:
+            fork = getattr(r, "fork", None)
+            c = self.__dict__["_rng_g"] = (r, fork(1) if fork is not None else r)
+        return c[1]
+
     def _generate(self, z):
         hub = getattr(self.generator, "noise_hub", None)      # G13_5's in-forward noise (progan has none)
         if hub is not None:
-            hub.source = self.rng.noise
-            hub.bulk_source = getattr(self.rng, "noise_bulk", None)   # DeviceRNG: one draw per forward
+            hub.attach(self.rng_g)
         return self.generator(z)
 
     def generator_trainstep(self, b_size):
@@ -81,7 +92,7 @@ class Train(CheckpointMixin):
     def generator_backward(self, b_size):
         """generator_trainstep up to (not including) the optimizer step."""
         self.optimizer_G.zero_grad()
-        z = self.rng.randn((b_size, self.nz, 1, 1))
+        z = self.rng_g.randn((b_size, self.nz, 1, 1))
         gen_imgs = self._generate(z)
         with _frozen(self.discriminator):
             g_loss = -torch.mean(self.discriminator(gen_imgs))
@@ -126,21 +137,14 @@ class Train(CheckpointMixin):
         depends on the generator's weights only, so a data-parallel driver may compute the NEXT
         critic step's batch on a second stream while this step's gradient all-reduce and
         optimizer update run (bench.py)."""
-        z = self.rng.randn((b_size, self.nz, 1, 1))
+        z = self.rng_g.randn((b_size, self.nz, 1, 1))
         with torch.no_grad():
             return self._generate(z)
-
-    # critic pass on the real batch concurrently with the fake batch's G forward (second stream):
-    # measured 36.7 vs 37.2 img/s -- the separate B-sized real and fake passes lose more GEMM
-    # efficiency than the overlap wins -- so off by default (A/B knob)
-    overlap_real = False
 
     def discriminator_backward(self, images, b_size, gen_imgs=None):
         """discriminator_trainstep up to (not including) the optimizer step.  ``gen_imgs``: a fake
         batch made beforehand by generate_fake (default: made here, in the reference's order)."""
         self.optimizer_D.zero_grad()
-        if gen_imgs is None and self.overlap_real and images.is_cuda:
-            return self._discriminator_backward_overlapped(images, b_size)
         if gen_imgs is None:
             gen_imgs = self.generate_fake(b_size)
         gen_imgs.requires_grad_()
@@ -154,32 +158,6 @@ class Train(CheckpointMixin):
         real_loss = -torch.mean(pred_r)
         fake_loss = torch.mean(pred_f)
         (real_loss + fake_loss).backward()
-        gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
-        gp.backward()
-        return real_loss, fake_loss, gp
-
-    def _discriminator_backward_overlapped(self, images, b_size):
-        """The reference's order of work (wgangp.py:58-66: G forward under no_grad, critic on the real
-        batch, critic on the fake batch, their backward calls accumulating) with the real-batch pass
-        issued on a second HIP stream while the generator's forward -- hundreds of small,
-        launch-bound kernels -- runs on the current one: the critic's large GEMMs fill the CUs the
-        generator leaves idle.  The real and fake passes are the reference's two separate calls
-        (their MiniBatchStdDev statistics are per call); the fake pass starts after the real one
-        has finished writing the shared gradient buffer."""
-        main = torch.cuda.current_stream()
-        side = getattr(self, "_side_stream", None)
-        if side is None or side.device != images.device:
-            side = self._side_stream = torch.cuda.Stream(device=images.device)
-        side.wait_stream(main)                   # zeroed gradients, the real batch
-        with torch.cuda.stream(side):
-            pred_r = self.discriminator(images)
-            real_loss = -torch.mean(pred_r)
-            real_loss.backward()
-        gen_imgs = self.generate_fake(b_size)    # current stream, concurrently
-        main.wait_stream(side)
-        pred_f = self.discriminator(gen_imgs.detach())
-        fake_loss = torch.mean(pred_f)
-        fake_loss.backward()
         gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
         gp.backward()
         return real_loss, fake_loss, gp

@@ -64,7 +64,7 @@ class Train(wgangp.Train):
 
     def discriminator_backward(self, images, b_size, idx):
         self.optimizer_D.zero_grad()
-        z = self.rng.randn((b_size, self.nz, 1, 1))
+        z = self.rng_g.randn((b_size, self.nz, 1, 1))
         plain = idx % LAZY_INTERVAL != 0
         with ops.math_mode(self.precision if plain else "fp32"), torch.no_grad():
             gen_imgs = self._generate(z)

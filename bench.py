@@ -56,10 +56,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the post-run breakdown and roofline probe (clean traces of the timed region)")
-    ap.add_argument("--no-bank", action="store_true", help="per-module style MLPs (A/B against the style bank)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="N>1: no second-stream fake-batch generation during the critic all-reduce (A/B)")
+                    help="one graph per phase, no second-stream fake-batch generation (A/B)")
     return ap.parse_args()
 
 
@@ -274,38 +273,38 @@ CONFIGS = {
 }
 
 
-def build(args, dev, rank):
-    """Models, trainer, and the iteration as a list of optimizer phases:
-    (graph key, backward callable, optimizer, images it consumes)."""
+def build(args, dev, rank, world):
+    """Models, trainer, and the timed iteration: a pipeline.Iteration for the WGAN-GP configs
+    (the tested graph schedule, tests/test_pipeline_gpu.py), else a list of optimizer phases
+    (graph key, backward callable, optimizer)."""
     import gan_amd
+    from gan_amd.pipeline import Iteration
     torch.manual_seed(1234)                         # identical initial weights on every rank
     if args.config == "progan":
         G = gan_amd.generator_3_progan.Generator(1, 256, 256, 3).to(dev)
         D = gan_amd.discriminator_3_wgangp_progan.Discriminator(1, 64, 3).to(dev)
     else:
         G = gan_amd.Generator(256).to(dev)
-        G.use_bank = not args.no_bank
         D = gan_amd.Discriminator().to(dev)
-    torch.cuda.manual_seed(4321 + rank)             # per-rank data / z / noise / eps stream
+    rng = gan_amd.DeviceRNG(dev, 4321 + rank)       # per-rank data / z / noise / eps streams
     if args.config == "lazy":
-        tr = gan_amd.wganlazygpR2.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev, 4321 + rank),
+        tr = gan_amd.wganlazygpR2.Train([], dev, 1, 256, G, args.config, D, args.config, rng=rng,
                                         precision=args.precision)
     else:
-        tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=gan_amd.DeviceRNG(dev, 4321 + rank))
+        tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=rng)
     B = args.batch
+    if args.config != "lazy":
+        return G, D, tr, Iteration(tr, B, N_CRITIC, world, overlap=not args.no_overlap)
+    data = rng.fork(2)
 
     def real():
-        return torch.randn(B, 3, 64, 64, device=dev)
+        return data.randn((B, 3, 64, 64))
 
-    gen = ("gen", lambda: tr.generator_backward(B), tr.optimizer_G, 0)
-    if args.config == "lazy":
-        phases = []
-        for idx in range(5):     # one lazy period: the regularised critic step, then 4 plain ones
-            key = "critic_reg" if idx == 0 else "critic"
-            phases += [(key, (lambda i=idx: tr.discriminator_backward(real(), B, i)), tr.optimizer_D, B), gen]
-    else:
-        crit = ("critic", lambda: tr.discriminator_backward(real(), B), tr.optimizer_D, B)
-        phases = [crit] * N_CRITIC + [gen]
+    gen = ("gen", lambda: tr.generator_backward(B), tr.optimizer_G)
+    phases = []
+    for idx in range(5):     # one lazy period: the regularised critic step, then 4 plain ones
+        key = "critic_reg" if idx == 0 else "critic"
+        phases += [(key, (lambda i=idx: tr.discriminator_backward(real(), B, i)), tr.optimizer_D), gen]
     return G, D, tr, phases
 
 
@@ -324,20 +323,21 @@ def main():
     from gan_amd import ops
     from gan_amd.dist import allreduce_mean_
 
-    G, D, tr, phases = build(args, dev, rank)
+    G, D, tr, it = build(args, dev, rank, world)
     B = args.batch
     headline = args.config == "wgangp"
+    pipelined = not isinstance(it, list)
     # images per iteration per GPU: the generator-step batches (wgangp: 1 per n_critic critic steps)
-    imgs_per_iter = B * sum(1 for k, *_ in phases if k == "gen")
-
-    def sync(opt):
-        if world > 1:
-            allreduce_mean_(opt.flat.grad)
+    imgs_per_iter = B if pipelined else B * sum(1 for k, *_ in it if k == "gen")
 
     def iteration():
-        for _key, bwd, opt, _ in phases:
+        if pipelined:
+            it.eager()
+            return
+        for _key, bwd, opt in it:
             bwd()
-            sync(opt)
+            if world > 1:
+                allreduce_mean_(opt.flat.grad)
             opt.step()
 
     # warm-up (eager); the first one also counts the conv FLOPs this build issues
@@ -356,108 +356,50 @@ def main():
 
     step = iteration
     graphs = {}
-    if args.mode == "graph":
+    if args.mode == "graph" and pipelined:
+        it.capture()
+        step = it.step
+        if rank == 0:
+            print(f"[bench] captured the iteration graphs ({'pipelined' if it.overlap else 'per phase'})",
+                  file=sys.stderr, flush=True)
+    elif args.mode == "graph":
         # one HIP graph per distinct phase (synthetic real batch, z, noise and eps are drawn
-        # inside; the device Philox stream offsets -- DeviceRNG's, and torch's for the real
-        # batch -- advance on every replay).  N = 1: backward + optimizer in one graph.  N > 1:
-        # the RCCL all-reduce of the flat gradient runs eagerly between a backward graph and an
-        # optimizer graph (collectives are kept out of capture).
-        # All phase graphs share ONE memory pool: the phases replay strictly one after another,
-        # so a later graph may reuse what an earlier one freed (per-graph pools would hold every
-        # phase's peak at once: > 250 GiB for the lazy config at B = 128).
+        # inside; the device Philox stream offsets advance on every replay).  N = 1: backward +
+        # optimizer in one graph.  N > 1: the all-reduce of the flat gradient runs eagerly between
+        # a backward graph and an optimizer graph (collectives are kept out of capture).  All
+        # phase graphs share ONE memory pool (they replay one after another).
         pool = torch.cuda.graph_pool_handle()
         torch.cuda.empty_cache()
 
-        def capture(fn, gpool=None):
+        def capture(fn):
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 fn()
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool if gpool is None else gpool):
+            with torch.cuda.graph(g, pool=pool):
                 fn()
             return g
 
-        if args.config == "wgangp" and not args.no_overlap:
-            # Critic steps with the overlap SURVEY.md §8(e)(2) allows: the next critic step's fake
-            # batch (no-grad G forward, 41 % of a critic step's FLOPs) depends on G's weights
-            # only -- G does not change during the n_critic steps -- so it runs on a second
-            # stream while this step's critic passes, gradient penalty, (N > 1: RCCL all-reduce)
-            # and AdamW run on the main stream; the generator's many small launch-bound kernels
-            # then share the GPU with the critic's large GEMMs.  The work per iteration is
-            # unchanged (5 generator forwards, 5 critic steps, 1 generator step); only the z /
-            # noise draws of the next step come before this step's eps draw.  The fake-batch
-            # graph has its own memory pool (it replays concurrently with others).
-            fake = {}
+        for key, bwd, opt in it:
+            if key in graphs:
+                continue
+            if world == 1:
+                graphs[key] = (capture(lambda b=bwd, o=opt: (b(), o.step())), None, opt)
+            else:
+                graphs[key] = (capture(bwd), capture(opt.step), opt)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] captured {len(graphs)} phase graphs", file=sys.stderr, flush=True)
 
-            def gfwd():
-                fake["x"] = tr.generate_fake(B)
-
-            g_fwd = capture(gfwd, torch.cuda.graph_pool_handle())
-            g_fwd.replay()                       # a valid fake batch for the captures below
-            g_crit = capture(lambda: tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B,
-                                                               gen_imgs=fake["x"]))
-            g_dstep = capture(tr.optimizer_D.step)
-            g_gen = capture(lambda: tr.generator_backward(B))
-            g_gstep = capture(tr.optimizer_G.step)
-            graphs = {"fake": (g_fwd, None, None), "critic": (g_crit, g_dstep, tr.optimizer_D),
-                      "gen": (g_gen, g_gstep, tr.optimizer_G)}
-            side = torch.cuda.Stream()
-            torch.cuda.synchronize()
-            if rank == 0:
-                print("[bench] captured the pipelined critic-step graphs", file=sys.stderr, flush=True)
-
-            fake_next = {}
-
-            def gfwd_next():
-                fake_next["x"] = tr.generate_fake(B)
-
-            # double-buffered fake batch: the side stream writes buffer (i+1)%2 while the critic
-            # reads buffer i%2 (a second captured copy of the generator forward, its own pool)
-            g_fwd2 = capture(gfwd_next, torch.cuda.graph_pool_handle())
-            g_fwd2.replay()
-            g_crit2 = capture(lambda: tr.discriminator_backward(torch.randn(B, 3, 64, 64, device=dev), B,
-                                                                gen_imgs=fake_next["x"]))
-            fwd_graphs, crit_graphs = (g_fwd, g_fwd2), (g_crit, g_crit2)
-            torch.cuda.synchronize()
-
-            def step():
-                cur = torch.cuda.current_stream()
-                fwd_graphs[0].replay()           # G changed in the previous generator step
-                for i in range(N_CRITIC):
-                    if i + 1 < N_CRITIC:         # the next step's fake batch, concurrently
-                        side.wait_stream(cur)    # (its buffer was last read two steps ago)
-                        with torch.cuda.stream(side):
-                            fwd_graphs[(i + 1) % 2].replay()
-                    crit_graphs[i % 2].replay()
-                    if world > 1:
-                        allreduce_mean_(tr.optimizer_D.flat.grad)
-                    g_dstep.replay()
-                    cur.wait_stream(side)
-                g_gen.replay()
-                if world > 1:
-                    allreduce_mean_(tr.optimizer_G.flat.grad)
-                g_gstep.replay()
-        else:
-            for key, bwd, opt, _ in phases:
-                if key in graphs:
-                    continue
-                if world == 1:
-                    graphs[key] = (capture(lambda b=bwd, o=opt: (b(), o.step())), None, opt)
-                else:
-                    graphs[key] = (capture(bwd), capture(opt.step), opt)
-            torch.cuda.synchronize()
-            if rank == 0:
-                print(f"[bench] captured {len(graphs)} phase graphs", file=sys.stderr, flush=True)
-
-            def step():
-                for key, *_ in phases:
-                    gb, go, opt = graphs[key]
-                    gb.replay()
-                    if go is not None:
-                        allreduce_mean_(opt.flat.grad)
-                        go.replay()
+        def step():
+            for key, *_ in it:
+                gb, go, opt = graphs[key]
+                gb.replay()
+                if go is not None:
+                    allreduce_mean_(opt.flat.grad)
+                    go.replay()
 
     if world > 1:
         dist.barrier()
@@ -480,14 +422,17 @@ def main():
 
     if rank == 0 and args.mode == "graph" and world == 1 and not args.no_extras:
         # breakdown (outside the timed region): one replay per phase graph
-        parts = {}
-        for key, (g, _, _) in graphs.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            g.replay()
-            e1.record()
-            torch.cuda.synchronize()
-            parts[key] = round(e0.elapsed_time(e1), 1)
+        if pipelined:
+            parts = it.phase_ms()
+        else:
+            parts = {}
+            for key, (g, _, _) in graphs.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                parts[key] = round(e0.elapsed_time(e1), 1)
         print(f"[bench] ms per phase graph: {parts}", file=sys.stderr, flush=True)
     probe = census = None
     if rank == 0 and world == 1 and headline and not args.no_extras:

@@ -367,6 +367,16 @@ int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float*
  * ------------------------------------------------------------------------------------- */
 int ganamd_philox_uniform(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream);
 int ganamd_philox_normal(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream);
+/* The general draw: counter word 1 = (g >> 32) + sub; advance != 0 advances *offset after the
+ * draw.  sub != 0 (then at most 2^34 elements) with advance = 0 lets several draws that may run
+ * concurrently on different streams share one offset word with distinct counters (a generator
+ * forward's per-draw noise inside ResnetInit's branch streams, generator_13_5.py:265,343-349);
+ * their owner calls ganamd_philox_advance once after joining them.  Consumers that run
+ * concurrently with each other own separate offset words (DeviceRNG.fork: word s starts at
+ * s * 2^40), so no two draws of an iteration share a counter. */
+int ganamd_philox_draw(float* out, long n, uint64_t seed, uint64_t* offset, uint32_t sub, int normal, int advance,
+                       hipStream_t stream);
+int ganamd_philox_advance(uint64_t* offset, hipStream_t stream);
 
 /* Library identification (for load checks). */
 const char* ganamd_version(void);

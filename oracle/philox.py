@@ -34,20 +34,21 @@ def philox4x32_10(ctr: np.ndarray, key: tuple[int, int]) -> np.ndarray:
     return np.stack(c, 1).astype(np.uint32)
 
 
-def words(n: int, seed: int, offset: int) -> np.ndarray:
-    """The first n words of a draw at stream offset `offset` (element 4g+i = word i of group g)."""
+def words(n: int, seed: int, offset: int, sub: int = 0) -> np.ndarray:
+    """The first n words of a draw at stream offset `offset` (element 4g+i = word i of group g);
+    `sub` is the draw index added to counter word 1 (csrc/rng.hip ganamd_philox_draw)."""
     g = np.arange((n + 3) // 4, dtype=np.uint64)
-    ctr = np.stack([g & _MASK, g >> np.uint64(32), np.full_like(g, offset & 0xFFFFFFFF),
+    ctr = np.stack([g & _MASK, (g >> np.uint64(32)) + np.uint64(sub), np.full_like(g, offset & 0xFFFFFFFF),
                     np.full_like(g, (offset >> 32) & 0xFFFFFFFF)], 1).astype(np.uint32)
     return philox4x32_10(ctr, (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)).reshape(-1)[:n]
 
 
-def uniform(n: int, seed: int, offset: int) -> np.ndarray:
-    return ((words(n, seed, offset) >> 8).astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float32)
+def uniform(n: int, seed: int, offset: int, sub: int = 0) -> np.ndarray:
+    return ((words(n, seed, offset, sub) >> 8).astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float32)
 
 
-def normal(n: int, seed: int, offset: int) -> np.ndarray:
-    w = words(4 * ((n + 3) // 4), seed, offset).reshape(-1, 2)
+def normal(n: int, seed: int, offset: int, sub: int = 0) -> np.ndarray:
+    w = words(4 * ((n + 3) // 4), seed, offset, sub).reshape(-1, 2)
     u1 = ((w[:, 0] >> 8).astype(np.float64) + 1.0) * 2.0 ** -24
     u2 = (w[:, 1] >> 8).astype(np.float64) * 2.0 ** -24
     r = np.sqrt(-2.0 * np.log(u1))

@@ -7,6 +7,12 @@ double backward) whose flat gradient is all-reduced (gan_amd.dist.allreduce_mean
 fused AdamW step, then a generator backward whose flat gradient is all-reduced too -- the order
 bench.py runs for N > 1.  Rank 0 writes the all-reduced gradients and the
 critic's parameters after its step to the path given as argv[1].
+
+``dp_worker.py OUT graph``: the bench's N > 1 graph-mode path instead -- one pipelined WGAN-GP
+iteration (gan_amd.pipeline.Iteration: captured fake-batch / critic / AdamW / generator graphs,
+the next fake batch on a side stream, the flat-gradient all-reduce eagerly between graphs) at
+B = 8 per rank with device Philox streams seeded per rank; rank 0 writes both models' parameters
+and gradients after the iteration.
 """
 import os
 import sys
@@ -18,6 +24,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 B = 4
+B_GRAPH = 8
+
+
+def graph_seed(rank):
+    return 960 + rank
 
 
 def shard_inputs(rank):
@@ -62,5 +73,34 @@ def main(out):
     dist.destroy_process_group()
 
 
+def main_graph(out):
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    import gan_amd
+    from gan_amd.pipeline import Iteration, restore, snapshot
+    dev = torch.device("cuda", 0)
+    G, D = make_models(gan_amd, dev)
+    tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev, graph_seed(rank)))
+    it = Iteration(tr, B_GRAPH, 5, world, overlap=True)
+    snap = snapshot(tr)
+    it.eager()                     # warm-up (all-reduces included), then capture
+    it.capture()
+    restore(tr, snap)
+    dist.barrier()
+    it.step()
+    torch.cuda.synchronize()
+    res = {k: v.detach().cpu().clone() for k, v in
+           (("g_data", tr.optimizer_G.flat.data), ("g_grad", tr.optimizer_G.flat.grad),
+            ("d_data", tr.optimizer_D.flat.data), ("d_grad", tr.optimizer_D.flat.grad))}
+    if rank == 0:
+        torch.save(dict(res, world=world), out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if len(sys.argv) > 2 and sys.argv[2] == "graph":
+        main_graph(sys.argv[1])
+    else:
+        main(sys.argv[1])

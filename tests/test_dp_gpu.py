@@ -7,8 +7,13 @@ one after another on the same weights and replayed random streams, their gradien
 by hand, and the critic update is applied from that mean.  The all-reduced gradients and the
 updated critic must match at 1e-5 (gloo sums the fp32 buffers on the host: one rounding).
 
+test_dp_graph_iteration_matches_shard_mean: the bench's N > 1 GRAPH-mode path (pipelined
+iteration, side-stream fake batches, all-reduce between captured graphs) on two ranks equals, after
+one full iteration (5 critic steps + generator step), the same iteration run here eagerly with the
+two shards one after another and their gradients averaged by hand before every optimizer step.
+
 test_bench_two_ranks: ``bench.py --gpus 2 --backend gloo`` starts its own ranks and reports
-n_gpus 2 (it used to run one rank silently).
+n_gpus 2 (it used to run one rank silently), in eager and in graph mode.
 """
 import json
 import os
@@ -80,9 +85,62 @@ def test_dp_steps_match_shard_mean(tmp_path):
     assert _rel(got["g_grad"], g_want) < 1e-5
 
 
-def test_bench_two_ranks():
+def test_dp_graph_iteration_matches_shard_mean(tmp_path):
+    out = str(tmp_path / "rank0_graph.pt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
+           "graph"]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert got["world"] == 2
+
+    import gan_amd
+    dev = torch.device("cuda", 0)
+    B = dp_worker.B_GRAPH
+    G, D = dp_worker.make_models(gan_amd, dev)
+    tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev, 1))
+    g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
+    with torch.no_grad():
+        tr.generate_fake(B)        # the workers' warm-up recorded the noise shapes: bulk draws from here
+    rngs = [gan_amd.DeviceRNG(dev, dp_worker.graph_seed(r)) for r in range(2)]
+
+    def mean_into(flat_grad, gs):
+        flat_grad.copy_(gs[0] + gs[1]).mul_(0.5)          # gloo: SUM, then * 1/N (dist.allreduce_mean_)
+
+    for _ in range(5):
+        gs = []
+        for rng in rngs:
+            tr.rng = rng
+            fake = tr.generate_fake(B)
+            tr.discriminator_backward(rng.fork(2).randn((B, 3, 64, 64)), B, gen_imgs=fake)
+            gs.append(tr.optimizer_D.flat.grad.detach().clone())
+        assert _rel(gs[0].cpu(), gs[1].cpu()) > 1e-2       # the shards really differ
+        mean_into(tr.optimizer_D.flat.grad, gs)
+        tr.optimizer_D.step()
+    gs = []
+    for rng in rngs:
+        tr.rng = rng
+        tr.generator_backward(B)
+        gs.append(tr.optimizer_G.flat.grad.detach().clone())
+    mean_into(tr.optimizer_G.flat.grad, gs)
+    tr.optimizer_G.step()
+    torch.cuda.synchronize()
+    want = {"g_data": tr.optimizer_G.flat.data, "g_grad": tr.optimizer_G.flat.grad,
+            "d_data": tr.optimizer_D.flat.data, "d_grad": tr.optimizer_D.flat.grad}
+    errs = {k: _rel(got[k], v.detach().cpu()) for k, v in want.items()}
+    # parameters relative to how far the iteration moved them
+    errs["g_move"] = float((got["g_data"] - want["g_data"].cpu()).double().norm() / (want["g_data"].cpu() - g0).double().norm())
+    errs["d_move"] = float((got["d_data"] - want["d_data"].cpu()).double().norm() / (want["d_data"].cpu() - d0).double().norm())
+    print("graph-mode DP vs shard mean:", errs)
+    assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
+    assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_bench_two_ranks(mode):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--batch", "8",
-           "--steps", "1", "--warmup", "1", "--mode", "eager", "--no-cpu-baseline", "--no-extras"]
+           "--steps", "1", "--warmup", "1", "--mode", mode, "--no-cpu-baseline", "--no-extras"]
     r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]

@@ -1,0 +1,127 @@
+"""The timed path is the tested path: bench.py's pipelined HIP-graph iteration (gan_amd.pipeline)
+against the same iteration run eagerly, and the device RNG's counter discipline under the
+concurrency that pipeline creates.
+
+test_pipelined_iteration_matches_eager  one replay of the captured iteration (fake batch of the
+    next critic step on a side stream, double-buffered; critic graphs; AdamW graphs; generator
+    step) and one eager iteration from the same state leave bit-identical parameters, gradients,
+    AdamW moments, BatchNorm statistics and RNG offsets; the eager run's draws never share a
+    Philox counter.
+test_branch_noise_draws                the first generator forward at a batch size draws its noise
+    per StyleConv inside ResnetInit's parallel branch streams: every draw reads the same offset
+    with its own draw index (checked against the numpy Philox oracle), and the offset advances
+    exactly once per forward.
+test_forks_concurrent                  two Philox streams drawing concurrently on two HIP streams
+    produce exactly their sequential oracle values.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import philox
+from tests import dp_worker
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+B = 8
+
+
+@pytest.fixture(scope="module")
+def gan():
+    import gan_amd
+    return gan_amd
+
+
+def _state(tr):
+    from gan_amd.pipeline import training_state
+    return [t.detach().clone() for t in training_state(tr)] + [o.clone() for o in tr.rng.state().values()]
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_pipelined_iteration_matches_eager(gan, overlap):
+    from gan_amd.pipeline import Iteration, restore, snapshot
+    G, D = dp_worker.make_models(gan, DEV)
+    tr = gan.Train([], DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.DeviceRNG(DEV, 2024))
+    it = Iteration(tr, B, n_critic=5, overlap=overlap)
+    it.eager()                      # warm-up: packed weights, noise shapes (bulk draws from here on)
+    torch.cuda.synchronize()
+    snap = snapshot(tr)
+    it.capture()                    # runs every phase once more eagerly, then captures
+    restore(tr, snap)
+    it.step()
+    torch.cuda.synchronize()
+    graph = _state(tr)
+
+    restore(tr, snap)
+    logs = []
+    for r in [tr.rng, tr.rng.fork(1), tr.rng.fork(2)]:
+        r.log = []
+        logs.append(r.log)
+    it.eager()
+    torch.cuda.synchronize()
+    for r in [tr.rng, tr.rng.fork(1), tr.rng.fork(2)]:
+        r.log = None
+    eager = _state(tr)
+
+    assert len(graph) == len(eager)
+    names = ["G.data", "G.grad", "G.m", "G.v", "G.step", "D.data", "D.grad", "D.m", "D.v", "D.step"]
+    for i, (a, b) in enumerate(zip(graph, eager)):
+        what = names[i] if i < len(names) else f"buffer/offset {i}"
+        assert torch.equal(a, b), f"{what}: pipelined replay differs from eager (max |d| {(a.double() - b.double()).abs().max()})"
+    # the iteration really moved the weights, and every draw had its own counter
+    assert not torch.equal(graph[0], snap[0][0]) and not torch.equal(graph[5], snap[0][5])
+    draws = [d for log in logs for d in log]
+    ctrs = [(s, off, sub) for s, off, sub, _ in draws]
+    assert len(set(ctrs)) == len(ctrs), "two draws of one iteration share a Philox counter"
+    kinds = {s for s, *_ in draws}
+    assert kinds == {0, 1, 2}, kinds            # eps, generator z + noise, real batches
+    # per iteration: 5 eps, 6 z + 6 bulk noise draws, 5 real batches
+    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 12, 5]
+
+
+def test_branch_noise_draws(gan):
+    G, _ = dp_worker.make_models(gan, DEV)
+    rng = gan.DeviceRNG(DEV, 99).fork(1)
+    got = []
+    inner = rng.noise_at
+
+    def rec(shape, idx):
+        t = inner(shape, idx)
+        got.append((idx, t))
+        return t
+    rng.noise_at = rec
+    G.noise_hub.attach(rng)
+    off0 = int(rng.offset.item())
+    with torch.no_grad():
+        G(torch.randn(4, 256, 1, 1, device=DEV))       # first forward at B = 4: per-draw noise
+    torch.cuda.synchronize()
+    assert int(rng.offset.item()) == off0 + 1
+    assert len(got) == 253 and [i for i, _ in got] == list(range(1, 254))
+    for idx, t in got[::23] + got[-1:]:
+        want = philox.normal(t.numel(), rng.seed, off0, idx)
+        np.testing.assert_allclose(t.reshape(-1).cpu().numpy(), want, rtol=1e-5, atol=1e-5)
+    # the next forward draws all of its noise in one bulk draw at the next offset
+    rng.noise_at = inner
+    with torch.no_grad():
+        G(torch.randn(4, 256, 1, 1, device=DEV))
+    torch.cuda.synchronize()
+    assert int(rng.offset.item()) == off0 + 2
+
+
+def test_forks_concurrent(gan):
+    base = gan.DeviceRNG(DEV, 5)
+    a, b = base.fork(1), base.fork(2)
+    assert a is base.fork(1) and a.stream == 1 and int(a.offset.item()) == 1 << 40
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    n, reps = 1 << 16, 20
+    outs = {1: [], 2: []}
+    for _ in range(reps):
+        with torch.cuda.stream(s1):
+            outs[1].append(a.randn((n,)))
+        with torch.cuda.stream(s2):
+            outs[2].append(b.rand((n,)))
+    torch.cuda.synchronize()
+    for k in range(0, reps, 7):
+        np.testing.assert_allclose(outs[1][k].cpu().numpy(), philox.normal(n, 5, (1 << 40) + k), rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(outs[2][k].cpu().numpy(), philox.uniform(n, 5, (2 << 40) + k))
+    assert int(a.offset.item()) == (1 << 40) + reps and int(b.offset.item()) == (2 << 40) + reps
