@@ -858,6 +858,268 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
   }
 }
 
+// ---- LDS-patch conv: stride 1, "same" padding, K x K taps (K = 3, 5), maps 32 / 64 wide ----------
+// The implicit GEMM above gathers its B operand per K-step straight from global memory: every
+// input pixel is fetched once per TAP (25 times for a 5x5 conv), which keeps the vector-memory
+// pipe ~half busy next to the MFMAs and needs 3 resident blocks per CU to hide the latency -- and
+// at 3 waves per SIMD the fp32 MFMA pipe sustains only ~111-120 TF/s on real data
+// (profiles/r02_mfma_ceiling_waves.txt; 154.5 at 1-2 waves).
+//
+// This kernel stages, per 16-channel chunk, the block's input PATCH with its halo --
+// P[(TH+K-1)(TW+K-1)][16], channel-minor -- in LDS once and runs all K*K taps of the chunk on it:
+// tap (kh, kw)'s B fragment of pixel (i, j) is patch position (i + kh, j + kw), read with the same
+// conflict-free [row][k] ds_read_b64 pattern as the GEMM's tiles.  Only the A operand (packed
+// weights, L2-resident) streams per K-step, two taps per barrier.  The patch is double-buffered:
+// the next chunk's patch is fetched into registers at the chunk's first tap pair and written to
+// the idle LDS buffer at the second, so the registers are free again for the rest of the chunk
+// and a chunk switch costs no extra barrier.  The x-scales of the modulated conv (x * s[c][b])
+// are folded into A while it is staged (b is fixed per block).
+//
+// Block: BM output channels x 512 pixels of ONE image (TH = 512 / TW rows of the full width
+// TW = W), 8 waves (wave w owns pixels 64w .. 64w + 63), one block per CU = 2 waves per SIMD, all
+// of the CU's LDS (2 patches + 2 A stages: <= 131 KB).  Block order: row tiles of one pixel
+// region run together (they share the patch in L2).
+constexpr int kPatchPix = 512, kPatchThreads = 512;
+
+template <int BM, int KK, int TW, bool BSCALE, bool ZERO>
+__global__ __launch_bounds__(kPatchThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void conv_patch_kernel(ConvArgs p) {
+  constexpr int NT = kPatchThreads;
+  constexpr int MB = (BM % 32 == 0) ? 32 : 16;          // MFMA block edge (48 rows: 16x16x4)
+  constexpr int TM = BM / MB, TN = 64 / MB, NR = MB == 32 ? 16 : 4;
+  using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
+  constexpr int TH = kPatchPix / TW, PAD = (KK - 1) / 2, T = KK * KK, NPAIR = (T + 1) / 2;
+  constexpr int PW = TW + KK - 1, NPOS = (TH + KK - 1) * PW;
+  constexpr int SPR = BK / 4, A4 = 2 * BM * SPR;          // 16-byte slots of a two-tap A stage
+  constexpr int EA = (A4 + NT - 1) / NT;
+  constexpr int AST = BM * LDK;                           // floats per tap in an A stage
+  __shared__ __attribute__((aligned(16))) float Ps[2][NPOS * LDK];
+  __shared__ __attribute__((aligned(16))) float As[2][2 * AST];
+  __shared__ __attribute__((aligned(16))) float Ss[2][BK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const Gather& g = p.g;
+  const int H = g.H, W = g.W, HW = H * W;
+  const int ty = blockIdx.x % p.gy, reg = blockIdx.x / p.gy;
+  const int tiles_img = H / TH;
+  const int b = reg / tiles_img, oh0 = (reg - b * tiles_img) * TH;
+  const int m0 = ty * BM;
+  const int nct = p.Ckp / BK;
+
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
+  const unsigned cs4 = 4u * (unsigned)(g.B * HW);       // one channel row of the source
+
+  // The patch is fetched in units of 4 channels at one position, u = cg * NPOS + pos (pos fastest:
+  // consecutive lanes read consecutive columns; a unit's 4 loads differ by a constant channel
+  // stride, and it lands in LDS as two ds_write_b64).  Threads past the last unit redo unit
+  // NU - 1 (same values, same LDS words).  u is made opaque so its index math is redone per
+  // chunk instead of being hoisted into live registers.
+  constexpr int NU = NPOS * (BK / 4), UPT = (NU + NT - 1) / NT;
+  auto patch_load = [&](int cc, f32x4 (&pv)[UPT]) {
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) {
+      int u = min(tid + e * NT, NU - 1);
+      asm volatile("" : "+v"(u));
+      const int cg = u / NPOS, pos = u - cg * NPOS;
+      const int pr = pos / PW, pc = pos - pr * PW;
+      int ih = oh0 - PAD + pr, iw = pc - PAD;
+      bool in = true;
+      if constexpr (ZERO) {
+        in = ih >= 0 && ih < H && iw >= 0 && iw < W;
+      } else {
+        ih = min(max(ih, 0), H - 1);
+        iw = min(max(iw, 0), W - 1);
+      }
+      // channels past the source's end fall outside the buffer: the hardware returns 0
+      const unsigned off = 4u * (unsigned)(b * HW + ih * W + iw) + (unsigned)(cc * BK + 4 * cg) * cs4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pv[e][q] = bload(rx, in ? (int)(off + q * cs4) : kOOB);
+    }
+  };
+  auto patch_store = [&](float* P, const f32x4 (&pv)[UPT]) {
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) {
+      int u = min(tid + e * NT, NU - 1);
+      asm volatile("" : "+v"(u));
+      const int cg = u / NPOS, pos = u - cg * NPOS;
+      float* d = P + pos * LDK + 4 * cg;
+      *reinterpret_cast<f32x2*>(d) = f32x2{pv[e][0], pv[e][1]};
+      *reinterpret_cast<f32x2*>(d + 2) = f32x2{pv[e][2], pv[e][3]};
+    }
+  };
+  // A stage of K-steps (cc, t0) and (cc, t0 + 1): slot -> (tap half, row, 4 k-values)
+  auto a_load = [&](int cc, int t0, f32x4 (&ra)[EA]) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int slot = min(tid + e * NT, A4 - 1);
+      const int half = slot / (BM * SPR), r = slot - half * (BM * SPR);
+      const int t = min(t0 + half, T - 1);
+      const int kt = cc * T + t;
+      ra[e] = bload4(rw, 4 * ((m0 + r / SPR) * (T * p.Ckp) + kt * BK + 4 * (r % SPR)));
+    }
+  };
+  // x-scales s[c][b] of chunk cc, 16 values (modulated conv)
+  auto s_load = [&](int cc) {
+    float v = 0.f;
+    if constexpr (BSCALE) v = bload(rsc, tid < BK ? 4 * ((cc * BK + tid) * g.B + b) : kOOB);
+    return v;
+  };
+  auto a_store = [&](float* A, const f32x4 (&ra)[EA], const float* S) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int slot = tid + e * NT;
+      if (EA * NT == A4 || slot < A4) {
+        const int half = slot / (BM * SPR), r = slot - half * (BM * SPR);
+        f32x4 v = ra[e];
+        if constexpr (BSCALE) v *= *reinterpret_cast<const f32x4*>(S + 4 * (r % SPR));
+        float* d = A + half * AST + (r / SPR) * LDK + 4 * (r % SPR);
+        *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
+        *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
+      }
+    }
+  };
+
+  // patch position of each of this lane's B columns at tap (0, 0)
+  int posb[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int q = wv * 64 + j * MB + (lane & (MB - 1));
+    posb[j] = (q / TW) * PW + q % TW;
+  }
+
+  acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
+
+  // One pair of taps as 4 (32x32x2) or 2 (16x16x4) half-steps of 8 k each: the LDS fragments of
+  // the next half-step are read while this one's MFMAs run (two fragment buffers), so only the
+  // first read after the pair's barrier is exposed.
+  //   32x32x2, half-step (tap t, hk): lane (r, h) supplies k = 8h + 4hk + s, s = 0..3
+  //   16x16x4, half-step = tap t:     lane (r, q) supplies k = 4q + s, s = 0..3
+  constexpr int HS = MB == 32 ? 2 : 1;                    // half-steps per tap
+  const int fr = MB == 32 ? (lane & 31) : (lane & 15);
+  const int fk = MB == 32 ? 8 * (lane >> 5) : 4 * (lane >> 4);
+  auto frag_read = [&](const float* __restrict__ A, const float* __restrict__ P, int toff, int hk,
+                       float (&fa)[TM][4], float (&fb)[TN][4]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* src = A + (i * MB + fr) * LDK + fk + 4 * hk;
+      const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
+      fa[i][0] = t0[0]; fa[i][1] = t0[1]; fa[i][2] = t1[0]; fa[i][3] = t1[1];
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* src = P + (posb[j] + toff) * LDK + fk + 4 * hk;
+      const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
+      fb[j][0] = t0[0]; fb[j][1] = t0[1]; fb[j][2] = t1[0]; fb[j][3] = t1[1];
+    }
+  };
+  auto frag_mfma = [&](const float (&fa)[TM][4], const float (&fb)[TN][4]) {
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (MB == 32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
+        }
+  };
+  constexpr auto toff = [](int t) { return (t / KK) * PW + t % KK; };
+
+  // prologue: chunk 0's patch and scales, the first A stage
+  {
+    f32x4 pv[UPT];
+    f32x4 ra[EA];
+    patch_load(0, pv);
+    a_load(0, 0, ra);
+    const float sv = s_load(0);
+    if (tid < BK) Ss[0][tid] = sv;
+    patch_store(Ps[0], pv);
+    __syncthreads();                                      // Ss[0] visible to a_store
+    a_store(As[0], ra, Ss[0]);
+  }
+  __syncthreads();
+  int ab = 0;
+  for (int cc = 0; cc < nct; ++cc) {
+    const int pb = cc & 1;
+    const float* P = Ps[pb];
+    const bool more_chunks = cc + 1 < nct;
+    f32x4 pv[UPT];
+    for (int pr = 0; pr < NPAIR; ++pr) {
+      const bool last = pr + 1 == NPAIR;
+      f32x4 ra[EA];
+      float sv = 0.f;
+      if (!last) {
+        a_load(cc, 2 * pr + 2, ra);
+      } else if (more_chunks) {
+        a_load(cc + 1, 0, ra);
+        sv = s_load(cc + 1);
+      }
+      if (pr == 0 && more_chunks) patch_load(cc + 1, pv);   // in flight during this chunk's first pair
+      const float* A = As[ab];
+      {
+        constexpr int NH = 2 * HS;                          // half-steps in a full pair
+        const int nh = (2 * pr + 1 < T) ? NH : HS;          // the odd last tap: one tap's
+        float fa[2][TM][4], fb[2][TN][4];
+        frag_read(A, P, toff(2 * pr), 0, fa[0], fb[0]);
+#pragma unroll
+        for (int q = 0; q < NH; ++q) {
+          if (q + 1 < nh) {
+            const int tq = (q + 1) / HS, hk = (q + 1) % HS;
+            frag_read(A + tq * AST, P, toff(2 * pr + tq), hk, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);              // keep the reads ahead of this half's MFMAs
+          if (q < nh) frag_mfma(fa[q & 1], fb[q & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (pr == 1 && more_chunks) patch_store(Ps[pb ^ 1], pv);   // the idle buffer (read last chunk)
+      if (last) {
+        if (!more_chunks) break;
+        if (NPAIR == 1) patch_store(Ps[pb ^ 1], pv);
+        if (tid < BK) Ss[pb ^ 1][tid] = sv;
+        __syncthreads();                                  // Ss[pb ^ 1] visible (and the patch)
+        a_store(As[ab ^ 1], ra, Ss[pb ^ 1]);
+      } else {
+        a_store(As[ab ^ 1], ra, Ss[pb]);
+      }
+      __syncthreads();
+      ab ^= 1;
+    }
+  }
+
+  // epilogue: the GEMM kernel's, with the block's pixel -> output column map
+  const int n_img = b * HW + oh0 * W;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int q = wv * 64 + j * MB + (lane & (MB - 1));
+    const int col = n_img + (q / TW) * W + q % TW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int m = m0 + i * MB + mfma_row<MB>(lane, r);
+        if (m >= p.M) continue;
+        float v = p.alpha * acc[i][j][r];
+        if (p.oscale) v *= p.oscale[m * g.B + b];
+        if (p.bias) v += p.bias[m];
+        if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
+        if (p.act) v = v > 0.f ? v : p.act[m] * v;
+        p.y[(long)m * p.ldy + col] = v;
+      }
+    }
+  }
+}
+
 // Batched repack: block b finds its job by binary search over the jobs' chunk offsets and packs
 // kPackChunk consecutive elements of that job's GEMM-order output.
 constexpr int kPackChunk = 4096;
@@ -1879,6 +2141,87 @@ hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
 
 // p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
 // GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
+// ---- patch-conv dispatch ----------------------------------------------------------------------
+int patch_enabled() {   // GANAMD_PATCH=0: every stride-1 conv through the gather GEMM (A/B)
+  static const int v = env_int("GANAMD_PATCH", 1);
+  return v;
+}
+
+template <int BM, int KK, int TW, bool BSCALE, bool ZERO>
+int patch_occ() {
+  static const int v = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_patch_kernel<BM, KK, TW, BSCALE, ZERO>, kPatchThreads, 0) !=
+            hipSuccess || n <= 0)
+      n = 1;
+    return n;
+  }();
+  return v;
+}
+
+template <int BM, int KK, int TW, bool BSCALE, bool ZERO>
+hipError_t launch_patch(ConvArgs p, hipStream_t st, bool dry, int* occ) {
+  if (occ) *occ = patch_occ<BM, KK, TW, BSCALE, ZERO>();
+  if (dry) return hipSuccess;
+  p.gy = (p.M + BM - 1) / BM;
+  const long blocks = (long)p.gy * p.g.B * (p.g.H / (kPatchPix / TW));
+  hipLaunchKernelGGL((conv_patch_kernel<BM, KK, TW, BSCALE, ZERO>), dim3((unsigned)blocks), dim3(kPatchThreads), 0, st,
+                     p);
+  return hipGetLastError();
+}
+
+template <int KK, int TW, bool BSCALE, bool ZERO>
+hipError_t patch_bm(const ConvArgs& p, int bm, hipStream_t st, bool dry, int* occ) {
+  switch (bm) {
+    case 48:
+      if constexpr (TW == 64) return launch_patch<48, KK, TW, BSCALE, ZERO>(p, st, dry, occ);
+      return hipErrorInvalidValue;
+    case 64: return launch_patch<64, KK, TW, BSCALE, ZERO>(p, st, dry, occ);
+    case 96: return launch_patch<96, KK, TW, BSCALE, ZERO>(p, st, dry, occ);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// The patch kernel's row tile: the packing tile (conv_bm, so the packed A is shared), except that
+// 128-row tiles run as two 64-row ones (128 accumulators per wave do not fit 2 waves per SIMD).
+int patch_bm_of(int M) {
+  const int bm = conv_bm(M);
+  return bm == 128 ? 64 : bm;
+}
+
+// The patch kernel's domain: stride 1, "same" padding (replicate or zero), square K = 3 / 5, the
+// full map width 32 or 64 as the tile width (TH = 256 / W rows per block), fp32, and enough blocks
+// for one full round of 2 per CU (smaller grids keep the gather GEMM with its split-K tails).
+bool patch_geometry(int M, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math) {
+  if (!patch_enabled() || math != GANAMD_MATH_F32 || stride != 1 || (K != 3 && K != 5) || pad != (K - 1) / 2 ||
+      OH != H || OW != W || (W != 32 && W != 64))
+    return false;
+  const int bm = patch_bm_of(M);
+  if (bm < 48 || (bm == 48 && W != 64)) return false;
+  const int th = kPatchPix / W;
+  if (H % th) return false;
+  // one block per CU: at least one full round, and the last round at least 3/4 full
+  const long blocks = (long)((M + bm - 1) / bm) * B * (H / th);
+  const long cus = num_cus(), rounds = (blocks + cus - 1) / cus;
+  return blocks >= cus && blocks >= 0.75 * rounds * cus;
+}
+
+template <bool ZERO>
+hipError_t dispatch_patch_z(const ConvArgs& p, int K, int bm, hipStream_t st, bool dry, int* occ) {
+  const bool s = p.g.scale != nullptr;
+  if (p.g.W == 64) {
+    if (K == 3) return s ? patch_bm<3, 64, true, ZERO>(p, bm, st, dry, occ) : patch_bm<3, 64, false, ZERO>(p, bm, st, dry, occ);
+    return s ? patch_bm<5, 64, true, ZERO>(p, bm, st, dry, occ) : patch_bm<5, 64, false, ZERO>(p, bm, st, dry, occ);
+  }
+  if (K == 3) return s ? patch_bm<3, 32, true, ZERO>(p, bm, st, dry, occ) : patch_bm<3, 32, false, ZERO>(p, bm, st, dry, occ);
+  return s ? patch_bm<5, 32, true, ZERO>(p, bm, st, dry, occ) : patch_bm<5, 32, false, ZERO>(p, bm, st, dry, occ);
+}
+
+hipError_t dispatch_patch(const ConvArgs& p, int K, hipStream_t st, bool dry = false, int* occ = nullptr) {
+  const int bm = patch_bm_of(p.M);
+  return p.g.mode == kZero ? dispatch_patch_z<true>(p, K, bm, st, dry, occ) : dispatch_patch_z<false>(p, K, bm, st, dry, occ);
+}
+
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
   const ConvPlan pl = conv_plan(p.M, p.N, p.Ck, p.T, p.g.mode, p.g.scale != nullptr, p.bf16 != 0);
   if ((pl.slab_elems && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
@@ -2111,12 +2454,26 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
   else
     dgrad_gemm(d, &M, &N, &Ck, &T);
   const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
+  if (op == GANAMD_CONV_FWD && !d->transposed && d->KH == d->KW &&
+      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math)) {
+    ConvArgs p{};
+    p.M = M;
+    p.g.W = d->W;
+    p.g.scale = scaled ? reinterpret_cast<const float*>(info) : nullptr;   // selects the instance only
+    p.g.mode = d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero;
+    int occ = 0;
+    (void)dispatch_patch(p, d->KH, nullptr, true, &occ);
+    const int bm = patch_bm_of(M), gy = (M + bm - 1) / bm, gx = d->B * (d->H / (kPatchPix / d->W));
+    const int v[11] = {bm, kPatchPix, gx, gy, gx, 1, ((Ck + BK - 1) / BK) * T, gx * gy, occ, num_cus(), 1};
+    for (int i = 0; i < 11; ++i) info[i] = v[i];
+    return GANAMD_OK;
+  }
   const ConvPlan pl = conv_plan(M, N, Ck, T, mode, scaled != 0, d->math == GANAMD_MATH_BF16);
-  const int v[10] = {pl.bm, pl.bn, pl.gx, pl.gy, pl.nfull_t, pl.S, pl.kt_per_split,
+  const int v[11] = {pl.bm, pl.bn, pl.gx, pl.gy, pl.nfull_t, pl.S, pl.kt_per_split,
                      pl.nfull_t * pl.gy + (pl.gx - pl.nfull_t) * pl.gy * pl.S,
                      conv_occupancy(pl.bm, pl.bn, mode, scaled, d->math == GANAMD_MATH_BF16),
-                     num_cus()};
-  for (int i = 0; i < 10; ++i) info[i] = v[i];
+                     num_cus(), 0};
+  for (int i = 0; i < 11; ++i) info[i] = v[i];
   return GANAMD_OK;
 }
 
@@ -2257,6 +2614,19 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
   float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))));
+  if (!d->transposed && p.g.mode != kTransposed &&
+      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math) && d->KH == d->KW) {
+    // LDS-patch conv (conv_patch_kernel): same packed A layout as the GEMM ([Mpad][T][Ckp])
+    const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
+    p.Ckp = (Ck + BK - 1) / BK * BK;
+    p.ldy = N;
+    if (!d->packed_w) {
+      launch_pack(ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, mpad, p.Ckp, 1, 0, 0, 0}, stream);
+      p.w = packed;
+    }
+    p.w_bytes = 4 * mpad * T * p.Ckp;
+    return dispatch_patch(p, d->KH, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  }
   if (!fwd_phased(d))
     return dispatch_conv(p, d->packed_w != 0, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   if (x_scale || y_scale) return GANAMD_EINVAL;   // phased transposed convs are unmodulated

@@ -640,6 +640,9 @@ __global__ __launch_bounds__(kNT) void row_dot_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) put_part(part, (long)c * S + s, acc, acc_mode);
 }
 
+// Plane reductions accumulate in double: they feed the modulated conv's style / demodulation
+// gradients, whose two paths nearly cancel (the output is invariant to a common scale of s), so
+// their rounding is amplified downstream (tests/test_headline_gpu.py::test_g_step_b16).
 // one wave per plane
 __global__ __launch_bounds__(kNT) void plane_dot_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                         long planes, long HW, float scale, float* __restrict__ out) {
@@ -648,38 +651,38 @@ __global__ __launch_bounds__(kNT) void plane_dot_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   for (long p = wave; p < planes; p += nwaves) {
     const float* ap = a + p * HW;
-    float acc = 0.f;
+    double acc = 0.0;
     if (b) {
       const float* bp = b + p * HW;
-      for (long i = lane; i < HW; i += 64) acc += ap[i] * bp[i];
+      for (long i = lane; i < HW; i += 64) acc += (double)ap[i] * bp[i];
     } else {
       for (long i = lane; i < HW; i += 64) acc += ap[i];
     }
-    acc = wave_sum(acc);
-    if (lane == 0) out[p] = scale * acc;
+    acc = wave_sum_d(acc);
+    if (lane == 0) out[p] = (float)(scale * acc);
   }
 }
 
 // planes of >= 1024 floats: a 256-thread block per plane, 16-byte loads
 __global__ __launch_bounds__(kNT) void plane_dot_big_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                             long HW, float scale, float* __restrict__ out) {
-  __shared__ float sh[4];
+  __shared__ double sh[4];
   typedef float f4 __attribute__((ext_vector_type(4)));
   const long p = blockIdx.x;
   const f4* a4 = reinterpret_cast<const f4*>(a + p * HW);
   const f4* b4 = b ? reinterpret_cast<const f4*>(b + p * HW) : nullptr;
-  float acc = 0.f;
+  double acc = 0.0;
   for (long i = threadIdx.x; i < HW / 4; i += kNT) {
     const f4 u = a4[i];
     if (b4) {
       const f4 v = b4[i];
-      acc += u[0] * v[0] + u[1] * v[1] + u[2] * v[2] + u[3] * v[3];
+      acc += (double)u[0] * v[0] + (double)u[1] * v[1] + (double)u[2] * v[2] + (double)u[3] * v[3];
     } else {
-      acc += u[0] + u[1] + u[2] + u[3];
+      acc += (double)u[0] + u[1] + u[2] + u[3];
     }
   }
-  acc = block_sum(acc, sh);
-  if (threadIdx.x == 0) out[p] = scale * acc;
+  acc = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) out[p] = (float)(scale * acc);
 }
 
 // Two plane dots sharing a: out1[p] = sum a*b1, out2[p] = sum a*b2 -- the modulated conv's
@@ -687,23 +690,23 @@ __global__ __launch_bounds__(kNT) void plane_dot_big_kernel(const float* __restr
 __global__ __launch_bounds__(kNT) void plane_dot_pair_kernel(const float* __restrict__ a, const float* __restrict__ b1,
                                                              const float* __restrict__ b2, long HW,
                                                              float* __restrict__ out1, float* __restrict__ out2) {
-  __shared__ float sh[4];
+  __shared__ double sh[4];
   typedef float f4 __attribute__((ext_vector_type(4)));
   const long p = blockIdx.x;
   const f4* a4 = reinterpret_cast<const f4*>(a + p * HW);
   const f4* c4 = reinterpret_cast<const f4*>(b1 + p * HW);
   const f4* d4 = reinterpret_cast<const f4*>(b2 + p * HW);
-  float s1 = 0.f, s2 = 0.f;
+  double s1 = 0.0, s2 = 0.0;
   for (long i = threadIdx.x; i < HW / 4; i += kNT) {
     const f4 u = a4[i], v = c4[i], w = d4[i];
-    s1 += u[0] * v[0] + u[1] * v[1] + u[2] * v[2] + u[3] * v[3];
-    s2 += u[0] * w[0] + u[1] * w[1] + u[2] * w[2] + u[3] * w[3];
+    s1 += (double)u[0] * v[0] + (double)u[1] * v[1] + (double)u[2] * v[2] + (double)u[3] * v[3];
+    s2 += (double)u[0] * w[0] + (double)u[1] * w[1] + (double)u[2] * w[2] + (double)u[3] * w[3];
   }
-  s1 = block_sum(s1, sh);
-  s2 = block_sum(s2, sh);
+  s1 = block_sum_d(s1, sh);
+  s2 = block_sum_d(s2, sh);
   if (threadIdx.x == 0) {
-    out1[p] = s1;
-    out2[p] = s2;
+    out1[p] = (float)s1;
+    out2[p] = (float)s2;
   }
 }
 

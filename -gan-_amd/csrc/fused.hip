@@ -31,6 +31,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 struct Ptr4 {
   const float* p[4];
 };
@@ -69,24 +75,26 @@ __global__ __launch_bounds__(kNT) void mix_bwd_kernel(Ptr4 f, const float* __res
   const int lane = threadIdx.x & 63;
   for (long p = wave; p < planes; p += nwaves) {
     const long base = p * HW;
-    float a[M], dot[M];
+    float a[M];
+    double dot[M];   // plane dots in double: the style gradient <g, x*...> cancels against the
+                     // demodulation path, so its rounding is amplified (tests/test_headline_gpu.py)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       a[m] = att[m * planes + p];
-      dot[m] = 0.f;
+      dot[m] = 0.0;
     }
     for (long i = lane; i < HW; i += 64) {
       const float gv = g[base + i];
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         if (gf.p[m]) gf.p[m][base + i] = gv * a[m];
-        dot[m] += gv * f.p[m][base + i];
+        dot[m] += (double)gv * f.p[m][base + i];
       }
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const float d = wave_sum(dot[m]);
-      if (lane == 0 && gatt) gatt[m * planes + p] = d;
+      const double d = wave_sum_d(dot[m]);
+      if (lane == 0 && gatt) gatt[m * planes + p] = (float)d;
     }
   }
 }
@@ -95,14 +103,15 @@ template <int M>
 __global__ __launch_bounds__(kNT) void mix_bwd_plane_kernel(Ptr4 f, const float* __restrict__ att, long planes,
                                                             long HW, const float* __restrict__ g, MPtr4 gf,
                                                             float* __restrict__ gatt) {
-  __shared__ float sh[M][4];
+  __shared__ double sh[M][4];
   const long p = blockIdx.x;
   const long base4 = p * HW / 4, n4 = HW / 4;
-  float a[M], dot[M];
+  float a[M];
+  double dot[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     a[m] = att[m * planes + p];
-    dot[m] = 0.f;
+    dot[m] = 0.0;
   }
   const f32x4* g4 = reinterpret_cast<const f32x4*>(g) + base4;
   for (long i = threadIdx.x; i < n4; i += kNT) {
@@ -111,19 +120,19 @@ __global__ __launch_bounds__(kNT) void mix_bwd_plane_kernel(Ptr4 f, const float*
     for (int m = 0; m < M; ++m) {
       if (gf.p[m]) reinterpret_cast<f32x4*>(gf.p[m])[base4 + i] = gv * a[m];
       const f32x4 fv = reinterpret_cast<const f32x4*>(f.p[m])[base4 + i];
-      dot[m] += gv[0] * fv[0] + gv[1] * fv[1] + gv[2] * fv[2] + gv[3] * fv[3];
+      dot[m] += (double)gv[0] * fv[0] + (double)gv[1] * fv[1] + (double)gv[2] * fv[2] + (double)gv[3] * fv[3];
     }
   }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    const float d = wave_sum(dot[m]);
+    const double d = wave_sum_d(dot[m]);
     if (lane == 0) sh[m][w] = d;
   }
   __syncthreads();
   if (threadIdx.x < M && gatt) {
     const int m = threadIdx.x;
-    gatt[m * planes + p] = sh[m][0] + sh[m][1] + sh[m][2] + sh[m][3];
+    gatt[m * planes + p] = (float)(sh[m][0] + sh[m][1] + sh[m][2] + sh[m][3]);
   }
 }
 

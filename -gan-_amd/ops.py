@@ -88,12 +88,12 @@ def math_mode(mode: str):
         _MATH[0] = prev
 
 
-PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus")
+PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus", "kernel")
 
 
 def plan_info(geo: "Geo", op: int, scaled: bool = False) -> dict:
     """The block schedule ganamd_conv_fwd / _dgrad launches for this geometry (ganamd_conv_plan_info)."""
-    info = (_lib.c_int * 10)()
+    info = (_lib.c_int * 11)()
     check(LIB.ganamd_conv_plan_info(geo.desc(), op, int(scaled), info), "conv_plan_info")
     return dict(zip(PLAN_FIELDS, list(info)))
 

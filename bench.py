@@ -144,49 +144,90 @@ def cpu_baseline(threads, B=8):
                       f"t_iter = 5*mean(t_D) + t_G = {t_iter:.1f}s"}
 
 
-# Dominant kernel: the implicit-GEMM conv kernel (conv_gemm_kernel, all instances ~55-65 % of the
-# iteration's GPU time; profiles/).  Representative launch: the critic's mid-level block conv --
-# D9_4 128->128 channels, 3x3 replication pad, 32x32 -- at B = 96: 768 output tiles = exactly one
-# round of the kernel's 3 resident blocks per CU, so the block schedule (ConvPlan) keeps whole
-# tiles and the call is ONE conv_gemm_kernel<128,128,2,2,1,false,false> launch (at the critic's
-# B = 128 it would add K-split tail blocks and a reduce launch).
-PROBE = dict(B=96, cin=128, h=32, cout=128, k=3)
+# Kernel rooflines (MFMA-bound).  Two launches are timed live, each on the
+# bench's current stream with its OWN pair of HIP events per launch (the per-dispatch duration a
+# rocprofv3 kernel trace reports; back-to-back launches also give the sustained rate):
+#   probe     D9_4's mid-level block conv, 128->128 channels, 3x3 replication pad, 32x32, at
+#             B = 96: 768 output tiles = one round of the kernel's resident blocks, so it is ONE
+#             conv_gemm_kernel<128,128,2,2,1,false,false> launch (whole tiles, no split-K);
+#   dominant  the kernel with the largest share of the iteration's GPU time in the rocprof trace:
+#             G13_5's 96-channel 5x5 modulated conv at 64x64 (x*s on the gather, *d in the
+#             epilogue), B = 64: conv_gemm_kernel<96,128,1,4,1,true,false>.
+PROBES = {
+    "probe": dict(B=96, cin=128, h=32, cout=128, k=3, scaled=False,
+                  shape="conv fwd B=96 128->128 3x3 replicate-pad 32x32 (D9_4 block conv; 768 whole tiles, one launch)"),
+    "dominant": dict(B=64, cin=96, h=64, cout=96, k=5, scaled=True,
+                     shape="modulated conv fwd B=64 96->96 5x5 replicate-pad 64x64 (G13_5 StyleConv; x*s gather, *d epilogue)"),
+}
 
 
-def roofline_probe(dev, reps=20):
+def probe_kernel(dev, spec, reps=20):
     import gan_amd.ops as ops
-    g = ops.conv_geo(PROBE["B"], PROBE["cin"], PROBE["h"], PROBE["h"], PROBE["cout"], PROBE["k"], 1, 1)
+    g = ops.conv_geo(spec["B"], spec["cin"], spec["h"], spec["h"], spec["cout"], spec["k"], 1, (spec["k"] - 1) // 2)
     x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
     w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
-    pl = ops.plan_info(g, 0, False)
-    assert pl["nfull_t"] == pl["gx"] and pl["S"] == 1, pl      # one launch, whole tiles
+    xs = torch.rand(g.Cin, g.B, device=dev) if spec["scaled"] else None
+    ys = torch.rand(g.Cout, g.B, device=dev) if spec["scaled"] else None
+    pl = ops.plan_info(g, 0, spec["scaled"])
+    assert pl["nfull_t"] == pl["gx"] and pl["S"] == 1, pl      # one launch, whole tiles (no split-K reduce)
+    if pl["kernel"] == 1:                                      # the LDS-patch conv (conv_gemm.hip)
+        kernel = f"conv_patch_kernel<{pl['bm']},{g.K},{g.W},{'true' if spec['scaled'] else 'false'}>"
+    else:
+        kernel = f"conv_gemm_kernel<{pl['bm']},{pl['bn']},...,{'true' if spec['scaled'] else 'false'},false>"
+    y = torch.empty(g.Cout, g.B, g.OH, g.OW, device=dev)
+
+    def launch():
+        ops._conv_fwd(g, x, w, None, xs, ys, 0.03, out=y)
     with torch.no_grad():
         for _ in range(3):
-            ops._conv_fwd(g, x, w, None, None, None, 0.03)   # packs the weight once (ops.PackCache)
-    torch.cuda.synchronize()
-    s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    with torch.no_grad():
-        for _ in range(reps):
-            ops._conv_fwd(g, x, w, None, None, None, 0.03)
-    e1.record(s)
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / reps
+            launch()                                         # packs the weight once (ops.PackCache)
+        torch.cuda.synchronize()
+        s = torch.cuda.current_stream()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in ev:                                    # one event pair per launch
+            e0.record(s)
+            launch()
+            e1.record(s)
+        torch.cuda.synchronize()
+        per = [e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):                                # back to back
+            launch()
+        e1.record(s)
+        torch.cuda.synchronize()
+    b2b = e0.elapsed_time(e1) * 1e3 / reps
+    us = sum(per) / len(per)
     flop = 2.0 * g.B * g.OH * g.OW * g.Cout * g.Cin * g.K * g.K
     tf = flop / us / 1e6
-    out = {"bound": "mfma", "kernel": "conv_gemm_kernel<128,128,2,2,1,false,false>",
-           "shape": "conv fwd B=96 128->128 3x3 replicate-pad 32x32 (D9_4 block conv; 768 whole tiles, one launch)",
-           "algorithmic_gflop_per_launch": flop / 1e9, "launch_us": us,
-           "achieved": tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP32_MFMA_PEAK_TFLOPS,
-           "traffic": None}
+    return {"bound": "mfma", "kernel": kernel, "shape": spec["shape"], "blocks": pl["blocks"],
+            "resident_blocks_per_cu": pl["occupancy"],
+            "algorithmic_gflop_per_launch": flop / 1e9, "launch_us": us, "launch_us_min": min(per),
+            "launch_us_back_to_back": b2b, "achieved": tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": tf / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+            "method": f"{reps} launches on the bench's stream, one HIP event pair each (mean); launch_us_back_to_back: "
+                      f"{reps} launches between two events"}
+
+
+def roofline_probe(dev):
+    """The line's roofline object is the DOMINANT kernel's; the critic probe rides along."""
+    out = probe_kernel(dev, PROBES["dominant"])
     # HBM bytes per launch from rocprofv3 PMC passes of this launch (tools/pmc_traffic.sh), if recorded
     tfile = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "roofline_traffic.json")
     if os.path.exists(tfile):
         t = json.load(open(tfile))
-        out["traffic"] = t.get("bytes_per_launch")
-        out["traffic_source"] = t.get("source")
+        if t.get("kernel") == out["kernel"]:
+            out["traffic"] = t.get("bytes_per_launch")
+            out["algorithmic_bytes_per_launch"] = t.get("algorithmic_bytes")
+            out["traffic_source"] = t.get("source")
+    out["critic_probe"] = probe_kernel(dev, PROBES["probe"])
     return out
+
+
+# Algorithmic GFLOP per image of each phase graph of the pipelined iteration (SURVEY.md §8(d)):
+# fake = the no-grad generator forward, critic = the rest of a critic step (critic on real + fake,
+# gradient penalty with its double backward), gen = the generator step.
+PHASE_GFLOP_PER_IMAGE = {"fake": 101.99, "critic": 245.93 - 101.99, "gen": 329.81}
 
 
 def bf16_algo(algo, issued, bf16_issued):
@@ -434,7 +475,14 @@ def main():
                 torch.cuda.synchronize()
                 parts[key] = round(e0.elapsed_time(e1), 1)
         print(f"[bench] ms per phase graph: {parts}", file=sys.stderr, flush=True)
+        phase_frac = None
+        if headline and pipelined and it.overlap:
+            phase_frac = {k: {"ms": v, "tflops": PHASE_GFLOP_PER_IMAGE[k] * B / v / 1e3,
+                              "frac": PHASE_GFLOP_PER_IMAGE[k] * B / v / 1e3 / FP32_MFMA_PEAK_TFLOPS}
+                          for k, v in parts.items() if k in PHASE_GFLOP_PER_IMAGE}
     probe = census = None
+    if "phase_frac" not in locals():
+        phase_frac = None
     if rank == 0 and world == 1 and headline and not args.no_extras:
         probe = roofline_probe(dev)
     if rank == 0 and world == 1 and not args.no_extras:
@@ -486,6 +534,8 @@ def main():
                                        "fp32 (157.3) / bf16 (2500) MFMA peaks weighted by the FLOPs each precision runs"}
         if census is not None:
             out["roofline"]["gemm_census"] = census
+        if phase_frac:
+            out["roofline"]["phases"] = phase_frac
         out["wall_s"] = wall
         if world == 1 and headline and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)

@@ -63,8 +63,9 @@ typedef struct ganamd_conv_desc {
 int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
 
 /* The block schedule conv_fwd / conv_dgrad will launch (introspection for tests and tools):
- * info[10] = {BM, BN, column tiles, row tiles, whole-tile columns, tail K-splits, K-steps per
- * split, blocks launched, resident blocks per CU of the instance, CUs}.  scaled: whether the
+ * info[11] = {BM, BN, column tiles, row tiles, whole-tile columns, tail K-splits, K-steps per
+ * split, blocks launched, resident blocks per CU of the instance, CUs, kernel (0: the gather
+ * GEMM, 1: the LDS-patch conv -- BN is then its 256-pixel region)}.  scaled: whether the
  * x_scale / gy_scale operand will be passed (it selects the kernel instance). */
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info);
 

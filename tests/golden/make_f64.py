@@ -245,7 +245,64 @@ def progan_main(trials=6):
     np.savez_compressed(os.path.join(HERE, "f64_progan.npz"), **out)
 
 
+def headline_main(trials=3):
+    """Generator steps above B=4 (train/wgangp.py:20-27):
+
+    * B=16: float64 truth of the reference's fixture g_step_b16.npz (make_golden_g16.py, same
+      seed 421), the reference's distance to it, and the fp32 spread (oracle in fp32 with ~1-ulp
+      perturbed weights) -> f64_g16.npz;
+    * B=64, the headline batch: the reference's own formulation does not fit this container there
+      (B x 178.7 M modulated weights kept for the backward: 47 GiB already at B=16), and neither
+      does the oracle's (~100 GiB); tests/test_headline_gpu.py::test_g_step_b64_vs_oracle runs the
+      fp32 oracle -- pinned to the reference at B=4 and B=16 -- on the GPU box's host instead."""
+    import resource
+    torch.set_num_threads(os.cpu_count() or 8)
+    pl = plan()
+    gnames = [n for n, _, _ in pl["g_params"]]
+    fx = fixture("g_step_b16.npz")
+    t0 = time.time()
+    smooth32 = om._SMOOTH
+    om._SMOOTH = smooth32.to(DT)
+    GP, DP = params64(pl["g_params"], pl["g_seed"]), params64(pl["d_params"], pl["d_seed"])
+    _gen, g_loss = om.WGANGP(GP, DP).generator_trainstep(16, Draw64(421))
+    om._SMOOTH = smooth32
+    rows = grad_rows(GP, gnames)
+    out = {"g16_loss": np.asarray([float(g_loss.detach())]), "g16_grads": rows,
+           "ref_g16_stats": np.asarray(grad_norm_stats(fx["grads"], rows)),
+           "ref_g16_loss_err": np.asarray(rel_err(fx["g_loss"], [float(g_loss.detach())]))}
+    del GP, DP, _gen, g_loss
+    print("g16 truth", time.time() - t0, out["ref_g16_stats"], out["ref_g16_loss_err"],
+          f"peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.1f} GiB", flush=True)
+
+    def fp32_step(B, seed, perturb):
+        GP = om.params_from_plan(pl["g_params"], pl["g_seed"])
+        DP = om.params_from_plan(pl["d_params"], pl["d_seed"])
+        if perturb:
+            g = torch.Generator().manual_seed(perturb)
+            with torch.no_grad():
+                for v in list(GP.t.values()) + list(DP.t.values()):
+                    v.mul_(1 + 6e-8 * torch.randn(v.shape, generator=g))
+        gen, g_loss = om.WGANGP(GP, DP).generator_trainstep(B, om.Draw(seed))
+        return float(g_loss.detach()), tensor_summary(gen.detach()), grad_rows(GP, gnames)
+
+    spread, lerr = [], []
+    for t in range(1, trials + 1):
+        l32, _, r32 = fp32_step(16, 421, t)
+        spread.append(grad_norm_stats(r32, rows))
+        lerr.append(rel_err([l32], out["g16_loss"]))
+        print("g16 spread", t, spread[-1], lerr[-1], flush=True)
+    out["g16_fp32_spread"], out["g16_loss_fp32_spread"] = np.asarray(spread), np.asarray(lerr)
+    np.savez_compressed(os.path.join(HERE, "f64_g16.npz"), **out)
+
+    # B=64 (the headline batch) is NOT written here: the oracle's fp32 generator step needs ~100 GiB
+    # of host memory there, beyond this container; tests/test_headline_gpu.py runs it on the GPU
+    # box's host inside the test, with bars from the B=16 spread above.
+
+
 if __name__ == "__main__":
+    if "--headline" in sys.argv:
+        headline_main()
+        sys.exit(0)
     if "--progan" in sys.argv:   # --trials N: fp32 draws for the spread (default 6; the fixture uses 24)
         progan_main(int(sys.argv[sys.argv.index("--trials") + 1]) if "--trials" in sys.argv else 6)
         sys.exit(0)

@@ -503,6 +503,51 @@ def test_conv_fwd_ex_noise_act(ops):
     assert rel(nc(got), y) < 1e-5
 
 
+PATCH_CASES = [
+    # B, Cin, H, Cout, k, pad mode, scaled, noise+act: shapes the LDS-patch conv takes
+    # (conv_patch_kernel: stride 1, "same" padding, 32/64-wide maps, >= 1 round of 1 block per CU)
+    (32, 96, 64, 96, 5, 1, True, True),      # G13_5 modulated 5x5 (96 rows: 32x32x2 blocks)
+    (32, 48, 64, 48, 3, 1, True, False),     # 48 rows: 16x16x4 blocks
+    (32, 40, 64, 45, 5, 0, False, False),    # ragged rows, channels not a multiple of 16, zero pad
+    (128, 128, 32, 128, 3, 1, False, False), # D9_4 block conv on the critic's 2B batch (two 64-row tiles)
+    (16, 108, 64, 108, 5, 1, False, True),   # the ToRGB pre-conv rows (128-row packing, 64-row tiles)
+    (128, 64, 32, 96, 5, 1, True, False),    # 32-wide map, 8-row regions
+]
+
+
+@pytest.mark.parametrize("case", PATCH_CASES)
+def test_conv_patch_kernel(ops, case):
+    B, Cin, H, Cout, k, mode, scaled, extra = case
+    p = (k - 1) // 2
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
+    pl = ops.plan_info(geo, 0, scaled)
+    assert pl["kernel"] == 1 and pl["occupancy"] >= 1, pl
+    g = torch.Generator().manual_seed(sum(case[:6]))
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64)
+    sx = torch.rand(Cin, B, generator=g, dtype=torch.float64) + 0.5 if scaled else None
+    sy = torch.rand(Cout, B, generator=g, dtype=torch.float64) + 0.5 if scaled else None
+    xm = x * sx.t()[:, :, None, None] if scaled else x
+    y = ref_conv(xm, w * 0.3, None, k, 1, p, mode)
+    if scaled:
+        y = y * sy.t()[:, :, None, None]
+    f = (lambda t: None if t is None else t.float().to(DEV))
+    nz = ns = al = None
+    if extra:
+        nz = torch.randn(Cout, B, H, H, generator=g, dtype=torch.float64)
+        ns = torch.rand(Cout, generator=g, dtype=torch.float64)
+        al = torch.rand(Cout, generator=g, dtype=torch.float64)
+        y = y + ns[None, :, None, None] * nz.permute(1, 0, 2, 3)
+        y = torch.where(y > 0, y, al[None, :, None, None] * y)
+    got = ops._conv_fwd_ex(geo, cn(x), f(w), f(sx), f(sy), 0.3, f(nz), f(ns), f(al))
+    assert rel(nc(got), y) < 1e-5
+    # persistent packed weights (Parameter): the same kernel on the GEMM-order copy
+    wp = torch.nn.Parameter(f(w))
+    got2 = ops._conv_fwd(geo, cn(x), wp, None, f(sx), f(sy), 0.3) if not extra else None
+    if got2 is not None:
+        assert rel(nc(got2), y) < 1e-5
+
+
 TAIL_CASES = [
     # B, Cin, H, Cout, k, pad: more output tiles than resident blocks, not a whole number of rounds
     (104, 128, 32, 128, 3, 1),

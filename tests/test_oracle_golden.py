@@ -299,3 +299,17 @@ def test_d_step_b64(P):
     assert rel_err(losses, fx["losses"]) < 1e-4
     rows, _ = _step_rows(DP, [n for n, k, _ in P["d_params"]])
     check_grads(rows, fx["grads"], D_BAR)
+
+
+@pytest.mark.skipif(not __import__("os").environ.get("GANAMD_SLOW"), reason="~1 min, ~25 GiB of CPU: set GANAMD_SLOW=1")
+def test_g_step_b16(P):
+    """The oracle's generator step at B=16 against the reference's (make_golden_g16.py): loss and
+    the gradient bars of tests/_util.G_BAR.  This pins the oracle that tests/test_headline_gpu.py
+    runs at B=64 (where neither the reference nor the oracle fits this container)."""
+    fx = fixture("g_step_b16.npz")
+    GP, DP = _g(P), _d(P)
+    tr = om.WGANGP(GP, DP)
+    _gen, g_loss = tr.generator_trainstep(16, om.Draw(421))
+    assert rel_err([float(g_loss.detach())], fx["g_loss"]) < 1e-4
+    rows, _ = _step_rows(GP, [n for n, k, _ in P["g_params"]])
+    print("oracle G-step B=16 vs reference", check_grads(rows, fx["grads"], G_BAR))

@@ -1,15 +1,19 @@
 #!/bin/bash
-# Effective shader clock and MFMA busy fraction of the tile-sweep GEMMs (rocprofv3 PMC pass).
-#   effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md, DVFS give-back)
+# Effective shader clock and MFMA utilisation of one conv shape (tools/gemm_micro.py args), for the
+# gather GEMM (GANAMD_PATCH=0) and the LDS-patch conv (GANAMD_PATCH=1), one rocprofv3 PMC pass each:
+#   clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md, DVFS give-back)
+#   util  = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x duration x clock)   (fp32 32x32x2: 64 cycles per MFMA)
+# TF/s = 157.3 x util x clock / 2.4 GHz: a kernel below peak is either clock-held (util high) or
+# issue-starved (util low).      usage: tools/clock_probe.sh TAG gemm_micro-args...
 set -e
+TAG=$1; shift
 export TMPDIR=/tmp
-rm -rf /tmp/prof_clk
-timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES --kernel-trace -d /tmp/prof_clk -o run --output-format csv -- python3 tools/tile_sweep.py > gpurun_out/clock_probe_run.log 2>&1
-C=$(find /tmp/prof_clk -name "*counter_collection.csv")
-K=$(find /tmp/prof_clk -name "*kernel_trace.csv")
-cp "$C" gpurun_out/clock_counters.csv
-cp "$K" gpurun_out/clock_trace.csv
-python3 - "$C" "$K" <<'PY'
+for P in 0 1; do
+  rm -rf /tmp/prof_clk_$TAG$P
+  GANAMD_PATCH=$P timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES --kernel-trace -d /tmp/prof_clk_$TAG$P -o run --output-format csv -- python3 tools/gemm_micro.py "$@" > /dev/null 2>&1
+  C=$(find /tmp/prof_clk_$TAG$P -name "*counter_collection.csv")
+  K=$(find /tmp/prof_clk_$TAG$P -name "*kernel_trace.csv")
+  python3 - "$C" "$K" "$P" <<'PY'
 import csv, sys, collections
 cnt = collections.defaultdict(dict)
 names = {}
@@ -19,10 +23,15 @@ for r in csv.DictReader(open(sys.argv[1])):
 dur = {}
 for r in csv.DictReader(open(sys.argv[2])):
     dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+rows = []
 for d in sorted(cnt):
-    if "gemm" not in names[d] or d not in dur or dur[d] < 1e-4:
+    if not ("gemm" in names[d] or "patch" in names[d]) or d not in dur or dur[d] < 1e-4:
         continue
     c = cnt[d]
-    clk = c.get("GRBM_GUI_ACTIVE", 0) / 8 / dur[d] / 1e9
-    print(f"{names[d][:60]:60s} {dur[d]*1e6:8.1f} us  clk {clk:5.2f} GHz  mfma_busy/gui {c.get('SQ_VALU_MFMA_BUSY_CYCLES',0)/max(1,c.get('GRBM_GUI_ACTIVE',1)):.3f}  busy_cu {c.get('SQ_BUSY_CU_CYCLES',0):.3g}")
+    clk = c.get("GRBM_GUI_ACTIVE", 0) / 8 / dur[d]
+    util = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (1024 * dur[d] * clk)
+    rows.append((names[d][:48], dur[d] * 1e6, clk / 1e9, util))
+for n, us, clk, u in rows[-3:]:
+    print(f"PATCH={sys.argv[3]} {n:48s} {us:8.1f} us  clk {clk:4.2f} GHz  mfma util {u:.3f}")
 PY
+done

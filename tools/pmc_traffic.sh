@@ -1,11 +1,11 @@
 #!/bin/bash
-# HBM traffic of bench.py's roofline-probe launch (conv_gemm_kernel<128,128,2,2,1,false,false>, conv fwd
-# B=96 128->128 3x3 32x32) from rocprofv3 PMC counters, one counter per pass (FETCH_SIZE and
+# HBM traffic of bench.py's roofline kernel -- the dominant one, conv_gemm_kernel<96,128,1,4,1,true,false>:
+# G13_5's modulated conv fwd B=64 96->96 5x5 64x64 -- from rocprofv3 PMC counters, one counter per pass (FETCH_SIZE and
 # WRITE_SIZE cannot share a pass on gfx950).  FETCH_SIZE is doubled (gfx950 reports half the bytes
 # of wide coalesced reads: MI355X_MICROARCH.md, HBM section).  Writes profiles/roofline_traffic.json.
 set -e
 export TMPDIR=/tmp
-ARGS="--op fwd --B 96 --cin 128 --H 32 --cout 128 --k 3 --pad 1 --reps 5"
+ARGS="--op fwd --B 64 --cin 96 --H 64 --cout 96 --k 5 --pad 2 --scaled --reps 5"
 for C in FETCH_SIZE WRITE_SIZE; do
   rm -rf /tmp/pmc_$C
   timeout -k 10 300 rocprofv3 --pmc $C -d /tmp/pmc_$C -o run --output-format csv -- python3 tools/gemm_micro.py $ARGS > /dev/null 2>&1
@@ -15,7 +15,7 @@ import csv, glob, json
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(f"/tmp/pmc_{c}/**/*counter_collection.csv", recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if "conv_gemm_kernel" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(f)) if "conv_gemm_kernel<96, 128, 1, 4, 1, true, false>" in r["Kernel_Name"]]
     per = {}
     for r in rows:
         per.setdefault(r["Dispatch_Id"], 0.0)
@@ -23,8 +23,10 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     vals[c] = sum(per.values()) / len(per)          # KiB per dispatch
 fetch_b = 2 * vals["FETCH_SIZE"] * 1024
 write_b = vals["WRITE_SIZE"] * 1024
-alg = 4 * (128 * 96 * 32 * 32 + 128 * 128 * 9 + 128 * 96 * 32 * 32)   # x read + W read + y write, once
-out = {"bytes_per_launch": fetch_b + write_b, "fetch_bytes_x2": fetch_b, "write_bytes": write_b,
+# x read + packed W read + x/y scales + y write, once
+alg = 4 * (96 * 64 * 64 * 64 + 96 * 96 * 25 + 2 * 96 * 64 + 96 * 64 * 64 * 64)
+out = {"kernel": "conv_gemm_kernel<96,128,1,4,1,true,false>",
+       "bytes_per_launch": fetch_b + write_b, "fetch_bytes_x2": fetch_b, "write_bytes": write_b,
        "raw_kib_per_dispatch": vals, "algorithmic_bytes": alg,
        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), tools/pmc_traffic.sh; FETCH doubled per the gfx950 correction"}
 json.dump(out, open("gpurun_out/roofline_traffic.json", "w"), indent=1)

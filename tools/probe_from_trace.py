@@ -1,9 +1,9 @@
-"""The roofline probe's launches in a rocprofv3 kernel trace of bench.py.
+"""The roofline probes' launches in a rocprofv3 kernel trace of bench.py.
 
-bench.py's probe issues 3 + 20 back-to-back launches of conv_gemm_kernel<128,128,2,2,1,false,false>
-at 768 blocks (D9_4's 128->128 3x3 conv at 32x32, B=96).  Other launches of that kernel can have
-768 blocks too (split-K tails, the census' 5-launch runs), so the probe is the run of >= 20
-consecutive dispatches (by start time) of that kernel and grid; its last 20 are averaged.
+bench.py times each roofline kernel (PROBES in bench.py) with 3 warm-up + 20 individually-timed
++ 20 back-to-back launches.  Other launches of those kernels with the same grid exist (the
+iteration's own, the census' 6-launch runs), so a probe is the longest run of >= 20 consecutive
+dispatches (by start time) of that kernel and grid; its launches after the first 3 are averaged.
 
     python tools/probe_from_trace.py TRACE.csv[.gz]
 """
@@ -11,26 +11,33 @@ import csv
 import gzip
 import sys
 
-KERNEL = "conv_gemm_kernel<128, 128, 2, 2, 1, false, false>"
+PROBES = [  # (kernel name as rocprof prints it, grid blocks, algorithmic GFLOP per launch, label)
+    ("conv_gemm_kernel<96, 128, 1, 4, 1, true, false>", 2048, 2.0 * 64 * 64 * 64 * 96 * 96 * 25 / 1e9,
+     "dominant: G13_5 modulated conv fwd B=64 96->96 5x5 64x64"),
+    ("conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", 768, 2.0 * 96 * 32 * 32 * 128 * 128 * 9 / 1e9,
+     "critic probe: D9_4 conv fwd B=96 128->128 3x3 32x32"),
+]
+PEAK = 157.3
+
 path = sys.argv[1]
 rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-best = []
-run = []
-for r in rows:
-    if KERNEL in r["Kernel_Name"] and int(r["Grid_Size_X"]) == 768 * 256:
-        run.append(r)
-    else:
-        if len(run) >= 20:
-            best = run
-        run = []
-if len(run) >= 20:
-    best = run
-if not best:
-    sys.exit("no run of >= 20 consecutive probe launches in the trace")
-last = best[-20:]
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
-avg = sum(d) / len(d)
-print(f"roofline probe: the last 20 of a run of {len(best)} back-to-back dispatches of {KERNEL} at 768 blocks")
-print(f"average {avg:.1f} us  min {min(d):.1f}  max {max(d):.1f}  -> {28.991029248e9 / (avg * 1e-6) / 1e12:.1f} TF/s "
-      f"(28.99 GFLOP per launch), {28.991029248e9 / (avg * 1e-6) / 1e12 / 157.3:.3f} of 157.3")
+for kernel, blocks, gflop, label in PROBES:
+    best, run = [], []
+    for r in rows:
+        if kernel in r["Kernel_Name"] and int(r["Grid_Size_X"]) == blocks * 256:
+            run.append(r)
+        else:
+            if len(run) > len(best):
+                best = run
+            run = []
+    if len(run) > len(best):
+        best = run
+    if len(best) < 20:
+        print(f"{label}: no run of >= 20 consecutive launches of {kernel} at {blocks} blocks")
+        continue
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in best[3:]]
+    avg = sum(d) / len(d)
+    print(f"{label}: {kernel} at {blocks} blocks, {len(d)} launches (run of {len(best)}, first 3 skipped)")
+    print(f"  average {avg:.1f} us  min {min(d):.1f}  max {max(d):.1f}  -> {gflop / avg * 1e-3 * 1e3:.1f} TF/s "
+          f"({gflop:.2f} GFLOP per launch), {gflop / avg * 1e3 / PEAK:.3f} of {PEAK}")
