@@ -52,6 +52,7 @@ _SIGS = {
     "ganamd_stream_capture_id": (c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_plan_info": (c_int, [ctypes.POINTER(ConvDesc), c_int, c_int, ctypes.POINTER(ctypes.c_int)]),
+    "ganamd_conv_set_patch": (c_int, [c_int]),
     "ganamd_conv_pack_bytes": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_pack_job": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, ctypes.POINTER(PackJob)]),
     "ganamd_pack_job_chunks": (ctypes.c_int64, [ctypes.POINTER(PackJob)]),
@@ -70,6 +71,8 @@ _SIGS = {
     "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
     "ganamd_rowreduce_workspace": (c_size_t, [c_int, c_long]),
     "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, vp]),
+    "ganamd_bn_act_fwd_seg": (c_int, [vp, c_int, c_long, c_int, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp,
+                                      vp, vp]),
     "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp]),
     "ganamd_prelu_fwd": (c_int, [vp, vp, c_int, c_long, vp, vp]),
     "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),

@@ -26,6 +26,7 @@
 // the prefetched registers are written to LDS.  Tiles are double buffered (one barrier per
 // K-step) and the next tile's gather is issued before the current tile's MFMAs.
 
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -133,6 +134,8 @@ __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int k
 // Output column of GEMM column n: the identity, or for one phase (qh, qw) of a stride-s transposed
 // conv n = (b, j, i) over the OHp x OWp phase grid -> (b, s*j + qh, s*i + qw) of the OH x OW output.
 //
+// s = -2 (ring only, the stride-1 dgrad next to conv_patch_kernel's interior): n = (b, ring position)
+// over B x Rn; the gather reads frame point ring_coord(position) and the result goes to `ring`.
 // s = -1 (frame split, the stride-1 dgrad): n = (b, a, c) over the (H+2p) x (W+2p) padded input
 // frame (ohwp = its size, OWp = its width, OW = W, OHW = H*W, qh = p, qw = H); interior positions
 // go straight to the input gradient, ring positions to `ring` ([row][b][Rn], Rn ring positions
@@ -155,6 +158,18 @@ __host__ __device__ __forceinline__ int ring_idx(int a, int c, int p, int H, int
   if (a < p) return a * Wp + c;
   if (a >= p + H) return (a - H) * Wp + c;
   return 2 * p * Wp + (a - p) * 2 * p + (c < p ? c : c - W);
+}
+// inverse of ring_idx: frame point (a, c) of ring position idx
+__host__ __device__ __forceinline__ void ring_coord(int idx, int p, int H, int W, int Wp, int& a, int& c) {
+  if (idx < 2 * p * Wp) {
+    const int r = idx / Wp;
+    c = idx - r * Wp;
+    a = r < p ? r : r + H;
+    return;
+  }
+  const int j = idx - 2 * p * Wp, r = j / (2 * p), q = j - r * (2 * p);
+  a = p + r;
+  c = q < p ? q : q + W;
 }
 // frame split: destination (base, row stride, column) of GEMM column n; false = not stored
 __device__ __forceinline__ bool frame_target(const OutMap& r, float* y, long ldy, int n, float*& base, long& ld,
@@ -479,8 +494,12 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
   if (n_ok) {
     bb = gn / p.ohw;
     const int rr = gn - bb * p.ohw;
-    oh = rr / g.OW;
-    ow = rr - oh * g.OW;
+    if (MODE == kTransposed && p.om.s == -2) {
+      ring_coord(rr, p.om.qh, p.om.qw, p.om.OW, p.om.OWp, oh, ow);
+    } else {
+      oh = rr / g.OW;
+      ow = rr - oh * g.OW;
+    }
   }
   const int img = bb * g.H * g.W;
   // per half: (channel chunk, tap) of its fp32 step f = 2*kt + half, advanced by 2 steps per K-step
@@ -602,8 +621,14 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
     long old = ldo, col = n;
     if (finish) {
       if constexpr (MODE == kPhase) col = out_col(p.om, n);
-      if constexpr (MODE == kTransposed)
-        if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) continue;
+      if constexpr (MODE == kTransposed) {
+        if (p.om.s == -2) {
+          obase = p.om.ring;
+          old = p.om.ldr;
+        } else if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) {
+          continue;
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
@@ -698,8 +723,12 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
   if (n_ok) {
     bb = gn / p.ohw;
     const int rr = gn - bb * p.ohw;
-    oh = rr / g.OW;
-    ow = rr - oh * g.OW;
+    if (MODE == kTransposed && p.om.s == -2) {
+      ring_coord(rr, p.om.qh, p.om.qw, p.om.OW, p.om.OWp, oh, ow);
+    } else {
+      oh = rr / g.OW;
+      ow = rr - oh * g.OW;
+    }
   }
   const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
   const int img = bb * g.H * g.W;
@@ -836,8 +865,14 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
     long old = ldo, col = n;
     if (finish) {
       if constexpr (MODE == kPhase) col = out_col(p.om, n);
-      if constexpr (MODE == kTransposed)
-        if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) continue;
+      if constexpr (MODE == kTransposed) {
+        if (p.om.s == -2) {
+          obase = p.om.ring;
+          old = p.om.ldr;
+        } else if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) {
+          continue;
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
@@ -860,42 +895,45 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
 
 // ---- LDS-patch conv: stride 1, "same" padding, K x K taps (K = 3, 5), maps 32 / 64 wide ----------
 // The implicit GEMM above gathers its B operand per K-step straight from global memory: every
-// input pixel is fetched once per TAP (25 times for a 5x5 conv), which keeps the vector-memory
-// pipe ~half busy next to the MFMAs and needs 3 resident blocks per CU to hide the latency -- and
-// at 3 waves per SIMD the fp32 MFMA pipe sustains only ~111-120 TF/s on real data
-// (profiles/r02_mfma_ceiling_waves.txt; 154.5 at 1-2 waves).
+// input pixel is fetched once per TAP (25 times for a 5x5 conv), and its LDS tiles need a block
+// barrier per K-step; at the 3 waves per SIMD it runs at, the fp32 MFMA pipe sustains ~111-120
+// TF/s on real data (profiles/r02_mfma_ceiling_waves.txt; 154.5 at 1-2 waves).
 //
 // This kernel stages, per 16-channel chunk, the block's input PATCH with its halo --
-// P[(TH+K-1)(TW+K-1)][16], channel-minor -- in LDS once and runs all K*K taps of the chunk on it:
-// tap (kh, kw)'s B fragment of pixel (i, j) is patch position (i + kh, j + kw), read with the same
-// conflict-free [row][k] ds_read_b64 pattern as the GEMM's tiles.  Only the A operand (packed
-// weights, L2-resident) streams per K-step, two taps per barrier.  The patch is double-buffered:
-// the next chunk's patch is fetched into registers at the chunk's first tap pair and written to
-// the idle LDS buffer at the second, so the registers are free again for the rest of the chunk
-// and a chunk switch costs no extra barrier.  The x-scales of the modulated conv (x * s[c][b])
-// are folded into A while it is staged (b is fixed per block).
+// P[(TH+K-1)(TW+K-1)][16], channel-minor -- in LDS once, and runs all K*K taps of the chunk on it:
+// tap (kh, kw)'s B fragment of pixel (i, j) is patch position (i + kh, j + kw), read with the
+// conflict-free [row][k] ds_read_b64 pattern of the GEMM's tiles.  The A operand (packed weights,
+// [Mpad][T][Ckp], the same few hundred KB for every block: L2/L1-resident) goes straight from
+// global memory into each wave's registers, one tap ahead -- no LDS stage and no barrier per
+// K-step: a block synchronises once per 16-channel CHUNK (25 taps of a 5x5 conv), when the
+// double-buffered patch swaps.  The next chunk's patch is fetched into registers during the
+// chunk's first tap and written to the idle buffer at its second, so those registers are free for
+// the rest of the chunk.  The modulated conv's x-scales s[c][b] (b is fixed per block) multiply
+// the A fragments in registers.
 //
 // Block: BM output channels x 512 pixels of ONE image (TH = 512 / TW rows of the full width
-// TW = W), 8 waves (wave w owns pixels 64w .. 64w + 63), one block per CU = 2 waves per SIMD, all
-// of the CU's LDS (2 patches + 2 A stages: <= 131 KB).  Block order: row tiles of one pixel
-// region run together (they share the patch in L2).
+// TW = W), 8 waves (wave w owns pixels 64w .. 64w + 63), one block per CU = 2 waves per SIMD.
+// Block order: row tiles of one pixel region run together (they share the patch in L2).
 constexpr int kPatchPix = 512, kPatchThreads = 512;
 
-template <int BM, int KK, int TW, bool BSCALE, bool ZERO>
+// DGRAD: the input gradient of a stride-1 "same" conv, interior of the padded frame: a zero-padded
+// correlation of gy with the taps reversed (A is the dgrad-packed weight [Cin][T][Cout]; tap t of
+// the forward is read as tap T-1-t); replication padding adds the frame's ring afterwards
+// (ganamd_conv_dgrad).
+template <int BM, int KK, int TW, bool BSCALE, bool DGRAD>
 __global__ __launch_bounds__(kPatchThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv_patch_kernel(ConvArgs p) {
+  constexpr bool ZERO = DGRAD;
   constexpr int NT = kPatchThreads;
   constexpr int MB = (BM % 32 == 0) ? 32 : 16;          // MFMA block edge (48 rows: 16x16x4)
   constexpr int TM = BM / MB, TN = 64 / MB, NR = MB == 32 ? 16 : 4;
+  constexpr int HS = MB == 32 ? 2 : 1;                    // half-steps (4 k per lane) per tap
+  constexpr int KPL = 4 * HS;                             // k values per lane per tap
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
-  constexpr int TH = kPatchPix / TW, PAD = (KK - 1) / 2, T = KK * KK, NPAIR = (T + 1) / 2;
+  constexpr int TH = kPatchPix / TW, PAD = (KK - 1) / 2, T = KK * KK;
   constexpr int PW = TW + KK - 1, NPOS = (TH + KK - 1) * PW;
-  constexpr int SPR = BK / 4, A4 = 2 * BM * SPR;          // 16-byte slots of a two-tap A stage
-  constexpr int EA = (A4 + NT - 1) / NT;
-  constexpr int AST = BM * LDK;                           // floats per tap in an A stage
+  constexpr int kPatchStoreTap = T > 4 ? 3 : T - 1;
   __shared__ __attribute__((aligned(16))) float Ps[2][NPOS * LDK];
-  __shared__ __attribute__((aligned(16))) float As[2][2 * AST];
-  __shared__ __attribute__((aligned(16))) float Ss[2][BK];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const Gather& g = p.g;
@@ -949,35 +987,29 @@ void conv_patch_kernel(ConvArgs p) {
       *reinterpret_cast<f32x2*>(d + 2) = f32x2{pv[e][2], pv[e][3]};
     }
   };
-  // A stage of K-steps (cc, t0) and (cc, t0 + 1): slot -> (tap half, row, 4 k-values)
-  auto a_load = [&](int cc, int t0, f32x4 (&ra)[EA]) {
+
+  // Lane fragment maps (k of this lane within a 16-deep K-step):
+  //   32x32x2: lane (r, h) supplies k = 8h + 4hk + s in half-step hk, step s = 0..3
+  //   16x16x4: lane (r, q) supplies k = 4q + s, s = 0..3 (one half-step per tap)
+  const int fr = MB == 32 ? (lane & 31) : (lane & 15);
+  const int fk = MB == 32 ? 8 * (lane >> 5) : 4 * (lane >> 4);
+  // A fragments of one tap from global memory: rows m0 + i*MB + fr, k = fk .. fk + KPL - 1
+  int a_off[TM];
 #pragma unroll
-    for (int e = 0; e < EA; ++e) {
-      const int slot = min(tid + e * NT, A4 - 1);
-      const int half = slot / (BM * SPR), r = slot - half * (BM * SPR);
-      const int t = min(t0 + half, T - 1);
-      const int kt = cc * T + t;
-      ra[e] = bload4(rw, 4 * ((m0 + r / SPR) * (T * p.Ckp) + kt * BK + 4 * (r % SPR)));
-    }
-  };
-  // x-scales s[c][b] of chunk cc, 16 values (modulated conv)
-  auto s_load = [&](int cc) {
-    float v = 0.f;
-    if constexpr (BSCALE) v = bload(rsc, tid < BK ? 4 * ((cc * BK + tid) * g.B + b) : kOOB);
-    return v;
-  };
-  auto a_store = [&](float* A, const f32x4 (&ra)[EA], const float* S) {
+  for (int i = 0; i < TM; ++i) a_off[i] = 4 * ((m0 + i * MB + fr) * (T * p.Ckp) + fk);
+  auto a_load = [&](int kt, f32x4 (&fa)[TM][HS]) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) {
-      const int slot = tid + e * NT;
-      if (EA * NT == A4 || slot < A4) {
-        const int half = slot / (BM * SPR), r = slot - half * (BM * SPR);
-        f32x4 v = ra[e];
-        if constexpr (BSCALE) v *= *reinterpret_cast<const f32x4*>(S + 4 * (r % SPR));
-        float* d = A + half * AST + (r / SPR) * LDK + 4 * (r % SPR);
-        *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
-        *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
-      }
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int hk = 0; hk < HS; ++hk) fa[i][hk] = bload4(rw, a_off[i] + kt * (BK * 4) + 16 * hk);
+  };
+  // x-scales of this lane's k values in chunk cc (modulated conv)
+  auto s_load = [&](int cc, f32x4 (&sv)[HS]) {
+    if constexpr (BSCALE) {
+#pragma unroll
+      for (int hk = 0; hk < HS; ++hk)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[hk][q] = bload(rsc, 4 * ((cc * BK + fk + 4 * hk + q) * g.B + b));
     }
   };
 
@@ -997,22 +1029,7 @@ void conv_patch_kernel(ConvArgs p) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 
-  // One pair of taps as 4 (32x32x2) or 2 (16x16x4) half-steps of 8 k each: the LDS fragments of
-  // the next half-step are read while this one's MFMAs run (two fragment buffers), so only the
-  // first read after the pair's barrier is exposed.
-  //   32x32x2, half-step (tap t, hk): lane (r, h) supplies k = 8h + 4hk + s, s = 0..3
-  //   16x16x4, half-step = tap t:     lane (r, q) supplies k = 4q + s, s = 0..3
-  constexpr int HS = MB == 32 ? 2 : 1;                    // half-steps per tap
-  const int fr = MB == 32 ? (lane & 31) : (lane & 15);
-  const int fk = MB == 32 ? 8 * (lane >> 5) : 4 * (lane >> 4);
-  auto frag_read = [&](const float* __restrict__ A, const float* __restrict__ P, int toff, int hk,
-                       float (&fa)[TM][4], float (&fb)[TN][4]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* src = A + (i * MB + fr) * LDK + fk + 4 * hk;
-      const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
-      fa[i][0] = t0[0]; fa[i][1] = t0[1]; fa[i][2] = t1[0]; fa[i][3] = t1[1];
-    }
+  auto b_read = [&](const float* __restrict__ P, int toff, int hk, float (&fb)[TN][4]) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const float* src = P + (posb[j] + toff) * LDK + fk + 4 * hk;
@@ -1020,7 +1037,10 @@ void conv_patch_kernel(ConvArgs p) {
       fb[j][0] = t0[0]; fb[j][1] = t0[1]; fb[j][2] = t1[0]; fb[j][3] = t1[1];
     }
   };
-  auto frag_mfma = [&](const float (&fa)[TM][4], const float (&fb)[TN][4]) {
+  auto mfma4 = [&](const f32x4 (&fa)[TM][HS], int hk, const f32x4 (&sv)[HS], const float (&fb)[TN][4]) {
+    f32x4 a[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = BSCALE ? fa[i][hk] * sv[hk] : fa[i][hk];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
@@ -1028,72 +1048,70 @@ void conv_patch_kernel(ConvArgs p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (MB == 32)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
           else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
         }
   };
-  constexpr auto toff = [](int t) { return (t / KK) * PW + t % KK; };
 
-  // prologue: chunk 0's patch and scales, the first A stage
+  // prologue: chunk 0's patch, tap 0's A fragments and the chunk's scales
+  f32x4 fa[2][TM][HS], sv[HS];
   {
     f32x4 pv[UPT];
-    f32x4 ra[EA];
     patch_load(0, pv);
-    a_load(0, 0, ra);
-    const float sv = s_load(0);
-    if (tid < BK) Ss[0][tid] = sv;
+    a_load(DGRAD ? T - 1 : 0, fa[0]);
+    s_load(0, sv);
     patch_store(Ps[0], pv);
-    __syncthreads();                                      // Ss[0] visible to a_store
-    a_store(As[0], ra, Ss[0]);
   }
   __syncthreads();
-  int ab = 0;
   for (int cc = 0; cc < nct; ++cc) {
-    const int pb = cc & 1;
-    const float* P = Ps[pb];
+    const float* P = Ps[cc & 1];
     const bool more_chunks = cc + 1 < nct;
     f32x4 pv[UPT];
-    for (int pr = 0; pr < NPAIR; ++pr) {
-      const bool last = pr + 1 == NPAIR;
-      f32x4 ra[EA];
-      float sv = 0.f;
-      if (!last) {
-        a_load(cc, 2 * pr + 2, ra);
-      } else if (more_chunks) {
-        a_load(cc + 1, 0, ra);
-        sv = s_load(cc + 1);
-      }
-      if (pr == 0 && more_chunks) patch_load(cc + 1, pv);   // in flight during this chunk's first pair
-      const float* A = As[ab];
-      {
-        constexpr int NH = 2 * HS;                          // half-steps in a full pair
-        const int nh = (2 * pr + 1 < T) ? NH : HS;          // the odd last tap: one tap's
-        float fa[2][TM][4], fb[2][TN][4];
-        frag_read(A, P, toff(2 * pr), 0, fa[0], fb[0]);
+    int kh = 0, kw = 0;
+#pragma unroll 1
+    for (int t = 0; t < T; t += 2) {
+      // two taps per iteration (register double buffer fa[0] / fa[1] without dynamic indexing)
 #pragma unroll
-        for (int q = 0; q < NH; ++q) {
-          if (q + 1 < nh) {
-            const int tq = (q + 1) / HS, hk = (q + 1) % HS;
-            frag_read(A + tq * AST, P, toff(2 * pr + tq), hk, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+      for (int u = 0; u < 2; ++u) {
+        const int tt = t + u;
+        if (tt < T) {
+          const int kt = cc * T + tt;
+          if (kt + 1 < nct * T) {                                    // next tap's weights
+            const int nt = (tt + 1 == T) ? 0 : tt + 1, nc = (tt + 1 == T) ? cc + 1 : cc;
+            a_load(nc * T + (DGRAD ? T - 1 - nt : nt), fa[u ^ 1]);
           }
-          __builtin_amdgcn_sched_barrier(0);              // keep the reads ahead of this half's MFMAs
-          if (q < nh) frag_mfma(fa[q & 1], fb[q & 1]);
-          __builtin_amdgcn_sched_barrier(0);
+          if (tt == 0 && more_chunks) patch_load(cc + 1, pv);      // next chunk's patch
+          const int toff = kh * PW + kw;
+          float fb[2][TN][4];
+          b_read(P, toff, 0, fb[0]);
+#pragma unroll
+          for (int hk = 0; hk < HS; ++hk) {
+            if (hk + 1 < HS) b_read(P, toff, hk + 1, fb[(hk + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma4(fa[u], hk, sv, fb[hk & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          // the idle buffer (last read in chunk cc - 1); a few taps after the loads were issued
+          if (tt == kPatchStoreTap && more_chunks) patch_store(Ps[(cc + 1) & 1], pv);
+          if (++kw == KK) {
+            kw = 0;
+            ++kh;
+          }
         }
       }
-      if (pr == 1 && more_chunks) patch_store(Ps[pb ^ 1], pv);   // the idle buffer (read last chunk)
-      if (last) {
-        if (!more_chunks) break;
-        if (NPAIR == 1) patch_store(Ps[pb ^ 1], pv);
-        if (tid < BK) Ss[pb ^ 1][tid] = sv;
-        __syncthreads();                                  // Ss[pb ^ 1] visible (and the patch)
-        a_store(As[ab ^ 1], ra, Ss[pb ^ 1]);
-      } else {
-        a_store(As[ab ^ 1], ra, Ss[pb]);
+      if (T % 2 == 1 && t + 2 > T) {
+        // odd tap count: the last tap used fa[0] and prefetched into fa[1]; realign
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int hk = 0; hk < HS; ++hk) fa[0][i][hk] = fa[1][i][hk];
       }
-      __syncthreads();
-      ab ^= 1;
+    }
+    if (more_chunks) {
+      if (T == 1) patch_store(Ps[(cc + 1) & 1], pv);
+      s_load(cc + 1, sv);
+      __syncthreads();            // chunk cc + 1's patch is complete; chunk cc's buffer is free
     }
   }
 
@@ -1832,7 +1850,10 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(
     const int n = n0 + (int)c;
     float* yb = y;
     long o;
-    if (!VEC && om.s < 0) {   // frame split (stride-1 dgrad): interior -> y, ring -> om.ring
+    if (!VEC && om.s == -2) {   // ring only: column n is the ring position
+      yb = om.ring;
+      o = (long)m * om.ldr + n;
+    } else if (!VEC && om.s < 0) {   // frame split (stride-1 dgrad): interior -> y, ring -> om.ring
       long ld, col;
       if (!frame_target(om, y, ldy, n, yb, ld, col)) continue;
       o = (long)m * ld + col;
@@ -2142,16 +2163,28 @@ hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
 // p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
 // GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
 // ---- patch-conv dispatch ----------------------------------------------------------------------
-int patch_enabled() {   // GANAMD_PATCH=0: every stride-1 conv through the gather GEMM (A/B)
-  static const int v = env_int("GANAMD_PATCH", 1);
+// GANAMD_PATCH bit 0: forward, bit 1: dgrad through the LDS-patch conv.  Off by default: faster in
+// isolation (96-ch 5x5 modconv 102 -> 111 TF/s, its dgrad 95 -> 101) but slower in the iteration
+// (41.4-42.0 img/s off vs 40.3-40.9 with either or both on, profiles/r03_ab_patch_iteration.txt):
+// its one 512-thread block per CU with a 117 KB LDS patch leaves no room for the kernels of the
+// concurrent streams (ResnetInit's branches, the side-stream fake batch) that the gather GEMM's
+// smaller blocks share the CUs with.
+std::atomic<int> g_patch{-1};
+
+int patch_enabled() {
+  int v = g_patch.load(std::memory_order_relaxed);
+  if (v < 0) {
+    v = env_int("GANAMD_PATCH", 0);
+    g_patch.store(v, std::memory_order_relaxed);
+  }
   return v;
 }
 
-template <int BM, int KK, int TW, bool BSCALE, bool ZERO>
+template <int BM, int KK, int TW, bool BSCALE, bool DGRAD>
 int patch_occ() {
   static const int v = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_patch_kernel<BM, KK, TW, BSCALE, ZERO>, kPatchThreads, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_patch_kernel<BM, KK, TW, BSCALE, DGRAD>, kPatchThreads, 0) !=
             hipSuccess || n <= 0)
       n = 1;
     return n;
@@ -2159,25 +2192,25 @@ int patch_occ() {
   return v;
 }
 
-template <int BM, int KK, int TW, bool BSCALE, bool ZERO>
+template <int BM, int KK, int TW, bool BSCALE, bool DGRAD>
 hipError_t launch_patch(ConvArgs p, hipStream_t st, bool dry, int* occ) {
-  if (occ) *occ = patch_occ<BM, KK, TW, BSCALE, ZERO>();
+  if (occ) *occ = patch_occ<BM, KK, TW, BSCALE, DGRAD>();
   if (dry) return hipSuccess;
   p.gy = (p.M + BM - 1) / BM;
   const long blocks = (long)p.gy * p.g.B * (p.g.H / (kPatchPix / TW));
-  hipLaunchKernelGGL((conv_patch_kernel<BM, KK, TW, BSCALE, ZERO>), dim3((unsigned)blocks), dim3(kPatchThreads), 0, st,
+  hipLaunchKernelGGL((conv_patch_kernel<BM, KK, TW, BSCALE, DGRAD>), dim3((unsigned)blocks), dim3(kPatchThreads), 0, st,
                      p);
   return hipGetLastError();
 }
 
-template <int KK, int TW, bool BSCALE, bool ZERO>
+template <int KK, int TW, bool BSCALE, bool DGRAD>
 hipError_t patch_bm(const ConvArgs& p, int bm, hipStream_t st, bool dry, int* occ) {
   switch (bm) {
     case 48:
-      if constexpr (TW == 64) return launch_patch<48, KK, TW, BSCALE, ZERO>(p, st, dry, occ);
+      if constexpr (TW == 64) return launch_patch<48, KK, TW, BSCALE, DGRAD>(p, st, dry, occ);
       return hipErrorInvalidValue;
-    case 64: return launch_patch<64, KK, TW, BSCALE, ZERO>(p, st, dry, occ);
-    case 96: return launch_patch<96, KK, TW, BSCALE, ZERO>(p, st, dry, occ);
+    case 64: return launch_patch<64, KK, TW, BSCALE, DGRAD>(p, st, dry, occ);
+    case 96: return launch_patch<96, KK, TW, BSCALE, DGRAD>(p, st, dry, occ);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2192,34 +2225,38 @@ int patch_bm_of(int M) {
 // The patch kernel's domain: stride 1, "same" padding (replicate or zero), square K = 3 / 5, the
 // full map width 32 or 64 as the tile width (TH = 256 / W rows per block), fp32, and enough blocks
 // for one full round of 2 per CU (smaller grids keep the gather GEMM with its split-K tails).
-bool patch_geometry(int M, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math) {
-  if (!patch_enabled() || math != GANAMD_MATH_F32 || stride != 1 || (K != 3 && K != 5) || pad != (K - 1) / 2 ||
+bool patch_geometry(int M, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math, bool dgrad) {
+  if (!(patch_enabled() & (dgrad ? 2 : 1)) || math != GANAMD_MATH_F32 || stride != 1 || (K != 3 && K != 5) || pad != (K - 1) / 2 ||
       OH != H || OW != W || (W != 32 && W != 64))
     return false;
   const int bm = patch_bm_of(M);
   if (bm < 48 || (bm == 48 && W != 64)) return false;
   const int th = kPatchPix / W;
   if (H % th) return false;
-  // one block per CU: at least one full round, and the last round at least 3/4 full
+  // one block per CU: whole rounds, or a last round at least 90 % full (a half-empty last round
+  // of these long blocks costs more than the gather GEMM's split-K tail: B = 96 critic probe,
+  // 384 blocks on 256 CUs, 97 vs 112 TF/s)
   const long blocks = (long)((M + bm - 1) / bm) * B * (H / th);
   const long cus = num_cus(), rounds = (blocks + cus - 1) / cus;
-  return blocks >= cus && blocks >= 0.75 * rounds * cus;
+  return blocks >= cus && blocks >= 0.9 * rounds * cus;
 }
 
-template <bool ZERO>
+template <bool DGRAD>
 hipError_t dispatch_patch_z(const ConvArgs& p, int K, int bm, hipStream_t st, bool dry, int* occ) {
   const bool s = p.g.scale != nullptr;
   if (p.g.W == 64) {
-    if (K == 3) return s ? patch_bm<3, 64, true, ZERO>(p, bm, st, dry, occ) : patch_bm<3, 64, false, ZERO>(p, bm, st, dry, occ);
-    return s ? patch_bm<5, 64, true, ZERO>(p, bm, st, dry, occ) : patch_bm<5, 64, false, ZERO>(p, bm, st, dry, occ);
+    if (K == 3) return s ? patch_bm<3, 64, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<3, 64, false, DGRAD>(p, bm, st, dry, occ);
+    return s ? patch_bm<5, 64, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<5, 64, false, DGRAD>(p, bm, st, dry, occ);
   }
-  if (K == 3) return s ? patch_bm<3, 32, true, ZERO>(p, bm, st, dry, occ) : patch_bm<3, 32, false, ZERO>(p, bm, st, dry, occ);
-  return s ? patch_bm<5, 32, true, ZERO>(p, bm, st, dry, occ) : patch_bm<5, 32, false, ZERO>(p, bm, st, dry, occ);
+  if (K == 3) return s ? patch_bm<3, 32, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<3, 32, false, DGRAD>(p, bm, st, dry, occ);
+  return s ? patch_bm<5, 32, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<5, 32, false, DGRAD>(p, bm, st, dry, occ);
 }
 
-hipError_t dispatch_patch(const ConvArgs& p, int K, hipStream_t st, bool dry = false, int* occ = nullptr) {
+// fwd: replication padding (every hot-path conv; zero-padded forwards keep the gather GEMM);
+// dgrad: the zero-padded, tap-reversed interior (ganamd_conv_dgrad)
+hipError_t dispatch_patch(const ConvArgs& p, int K, bool dgrad, hipStream_t st, bool dry = false, int* occ = nullptr) {
   const int bm = patch_bm_of(p.M);
-  return p.g.mode == kZero ? dispatch_patch_z<true>(p, K, bm, st, dry, occ) : dispatch_patch_z<false>(p, K, bm, st, dry, occ);
+  return dgrad ? dispatch_patch_z<true>(p, K, bm, st, dry, occ) : dispatch_patch_z<false>(p, K, bm, st, dry, occ);
 }
 
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
@@ -2446,6 +2483,12 @@ int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes) {
   return GANAMD_OK;
 }
 
+int ganamd_conv_set_patch(int mask) {
+  const int prev = patch_enabled();
+  if (mask >= 0) g_patch.store(mask & 3, std::memory_order_relaxed);
+  return prev;
+}
+
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info) {
   if (!desc_ok(d) || !info || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
   int M, N, Ck, T;
@@ -2454,15 +2497,15 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
   else
     dgrad_gemm(d, &M, &N, &Ck, &T);
   const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
-  if (op == GANAMD_CONV_FWD && !d->transposed && d->KH == d->KW &&
-      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math)) {
+  if (op == GANAMD_CONV_FWD && !d->transposed && d->KH == d->KW && d->pad_mode == GANAMD_PAD_REPLICATE &&
+      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, false)) {
     ConvArgs p{};
     p.M = M;
     p.g.W = d->W;
     p.g.scale = scaled ? reinterpret_cast<const float*>(info) : nullptr;   // selects the instance only
     p.g.mode = d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero;
     int occ = 0;
-    (void)dispatch_patch(p, d->KH, nullptr, true, &occ);
+    (void)dispatch_patch(p, d->KH, false, nullptr, true, &occ);
     const int bm = patch_bm_of(M), gy = (M + bm - 1) / bm, gx = d->B * (d->H / (kPatchPix / d->W));
     const int v[11] = {bm, kPatchPix, gx, gy, gx, 1, ((Ck + BK - 1) / BK) * T, gx * gy, occ, num_cus(), 1};
     for (int i = 0; i < 11; ++i) info[i] = v[i];
@@ -2513,8 +2556,13 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
              slab_bytes(M, N, Ck, T, fwd_mode(d), d->math == GANAMD_MATH_BF16);
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
+    // split slabs: the frame GEMM's, or the ring-only GEMM's next to the patch conv (B x ring columns)
+    const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
+    const int Nring = d->B * (Hp * Wp - d->H * d->W);
+    const size_t slabs = std::max(slab_bytes(M, N, Ck, T, dgrad_mode(d), d->math == GANAMD_MATH_BF16),
+                                  Nring > 0 ? slab_bytes(M, Nring, Ck, T, kTransposed, d->math == GANAMD_MATH_BF16) : 0);
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
-             align256(dgrad_scatter_bytes(d)) + slab_bytes(M, N, Ck, T, dgrad_mode(d), d->math == GANAMD_MATH_BF16);
+             align256(dgrad_scatter_bytes(d)) + slabs;
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
     T = d->KH * d->KW;
@@ -2614,8 +2662,8 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
   float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))));
-  if (!d->transposed && p.g.mode != kTransposed &&
-      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math) && d->KH == d->KW) {
+  if (!d->transposed && p.g.mode == kReplicate &&
+      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, false) && d->KH == d->KW) {
     // LDS-patch conv (conv_patch_kernel): same packed A layout as the GEMM ([Mpad][T][Ckp])
     const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
     p.Ckp = (Ck + BK - 1) / BK * BK;
@@ -2625,7 +2673,7 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
       p.w = packed;
     }
     p.w_bytes = 4 * mpad * T * p.Ckp;
-    return dispatch_patch(p, d->KH, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+    return dispatch_patch(p, d->KH, false, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   if (!fwd_phased(d))
     return dispatch_conv(p, d->packed_w != 0, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
@@ -2711,6 +2759,38 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   // frame in the epilogue (OutMap s = -1): interior -> gx, ring -> ring buffer (replication) or
   // dropped (zero padding); ring_fold_kernel then adds the ring onto the edge pixels.
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
+  if (d->KH == d->KW && patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, true)) {
+    // the frame's interior with the LDS-patch conv (zero-padded, taps reversed), then -- for
+    // replication padding -- the ring alone through the gather GEMM (OutMap s = -2) and its fold
+    const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
+    p.Ckp = (Ck + BK - 1) / BK * BK;
+    if (!pre) {
+      launch_pack(ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, mpad, p.Ckp, 1, 0, 0, 0}, stream);
+      p.w = packed;
+    }
+    p.w_bytes = 4 * mpad * T * p.Ckp;
+    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->H, d->W, d->KW, 1, d->pad, kZero};
+    p.y = gx;
+    p.N = d->B * d->H * d->W;
+    p.ohw = d->H * d->W;
+    p.ldy = p.N;
+    if (dispatch_patch(p, d->KH, true, stream) != hipSuccess) return GANAMD_ELAUNCH;
+    if (!pad_bytes) return GANAMD_OK;
+    float* ring = reinterpret_cast<float*>(ws);
+    const int Rn = Hp * Wp - d->H * d->W;
+    p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
+    p.N = d->B * Rn;
+    p.ohw = Rn;
+    p.om = OutMap{-2, d->pad, d->H, Wp, Hp * Wp, d->W, d->H * d->W, Rn, (long)d->B * Rn, ring};
+    p.ldy = p.N;
+    p.y = ring;
+    if (dispatch_conv(p, true, nullptr, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+    const long planes = (long)d->Cin * d->B;
+    const long edges = (long)2 * d->W + 2 * d->H;
+    hipLaunchKernelGGL(ring_fold_kernel, dim3(grid1d(planes * edges)), dim3(256), 0, stream, ring, gx, (int)planes,
+                       d->H, d->W, d->pad);
+    return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  }
   p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
   p.y = gx;
   p.ohw = Hp * Wp;

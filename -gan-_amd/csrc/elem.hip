@@ -105,10 +105,11 @@ __global__ __launch_bounds__(kNT) void bn_partial_kernel(const float* __restrict
 
 __device__ __forceinline__ void bn_store_stats(int c, double mean, double m2, long L, float* running_mean,
                                                float* running_var, float momentum, float eps, float* save_mean,
-                                               float* save_invstd) {
+                                               float* save_invstd, float* seg_uvar = nullptr) {
   const double var = m2 / (double)L;
   save_mean[c] = (float)mean;
   save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (seg_uvar) seg_uvar[c] = (float)(L > 1 ? m2 / (double)(L - 1) : var);   // segmented: running stats later
   if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
   if (running_var) {
     const float unb = (float)(L > 1 ? m2 / (double)(L - 1) : var);
@@ -146,9 +147,11 @@ __global__ __launch_bounds__(kNT) void bn_small_fwd_kernel(const float* __restri
                                                            const float* __restrict__ alpha, float* running_mean,
                                                            float* running_var, float momentum, float eps,
                                                            float* __restrict__ y, float* __restrict__ save_mean,
-                                                           float* __restrict__ save_invstd) {
+                                                           float* __restrict__ save_invstd, int seg,
+                                                           float* __restrict__ seg_uvar) {
   const int c = blockIdx.x * (kNT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= C) return;
+  const int pc = c / seg;   // segmented BatchNorm: row c = (channel pc, segment c % seg)
   const float* row = x + (long)c * L;
   float v[kSmallPer];
   double sum = 0.0;
@@ -167,8 +170,9 @@ __global__ __launch_bounds__(kNT) void bn_small_fwd_kernel(const float* __restri
   }
   m2 = wave_sum_d(m2);
   const float mu = (float)mean, is = (float)(1.0 / sqrt(m2 / L + (double)eps));
-  if (lane == 0) bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
-  const float ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  if (lane == 0)
+    bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd, seg_uvar);
+  const float ga = gamma[pc], be = beta[pc], al = alpha ? alpha[pc] : 1.f;
   float* yr = y + (long)c * L;
 #pragma unroll
   for (int j = 0; j < kSmallPer; ++j) {
@@ -246,9 +250,10 @@ __global__ __launch_bounds__(kNT) void bn_mid_fwd_kernel(const float* __restrict
                                                          const float* __restrict__ alpha, float* running_mean,
                                                          float* running_var, float momentum, float eps,
                                                          float* __restrict__ y, float* __restrict__ save_mean,
-                                                         float* __restrict__ save_invstd) {
+                                                         float* __restrict__ save_invstd, int seg,
+                                                         float* __restrict__ seg_uvar) {
   __shared__ double sh[kNT / 64];
-  const int c = blockIdx.x, tid = threadIdx.x;
+  const int c = blockIdx.x, tid = threadIdx.x, pc = c / seg;
   const float* row = x + (long)c * L;
   float v[kMidPer];
   double sum = 0.0;
@@ -267,8 +272,9 @@ __global__ __launch_bounds__(kNT) void bn_mid_fwd_kernel(const float* __restrict
   }
   m2 = block_sum_d(m2, sh);
   const float mu = (float)mean, is = (float)(1.0 / sqrt(m2 / L + (double)eps));
-  if (tid == 0) bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
-  const float ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+  if (tid == 0)
+    bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd, seg_uvar);
+  const float ga = gamma[pc], be = beta[pc], al = alpha ? alpha[pc] : 1.f;
   float* yr = y + (long)c * L;
 #pragma unroll
   for (int j = 0; j < kMidPer; ++j) {
@@ -414,8 +420,8 @@ __global__ __launch_bounds__(kNT) void bn_act_apply_stats_kernel(
     const float* __restrict__ x, long L, int S, const double* __restrict__ part, float* running_mean,
     float* running_var, float momentum, float eps, float* save_mean, float* save_invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ alpha,
-    float* __restrict__ y) {
-  const int c = blockIdx.y;
+    float* __restrict__ y, int seg, float* __restrict__ seg_uvar) {
+  const int c = blockIdx.y, pc = c / seg;
   const double* p = part + (long)c * S * 3;
   double n = 0, mean = 0, m2 = 0;
   for (int s = 0; s < S; ++s) {
@@ -429,8 +435,8 @@ __global__ __launch_bounds__(kNT) void bn_act_apply_stats_kernel(
   const float mu = (float)mean;
   const float is = (float)(1.0 / sqrt(m2 / (double)L + (double)eps));
   if (blockIdx.x == 0 && threadIdx.x == 0)
-    bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd);
-  const float ga = gamma[c], be = beta[c], al = alpha ? alpha[c] : 1.f;
+    bn_store_stats(c, mean, m2, L, running_mean, running_var, momentum, eps, save_mean, save_invstd, seg_uvar);
+  const float ga = gamma[pc], be = beta[pc], al = alpha ? alpha[pc] : 1.f;
   const long per = (L + gridDim.x - 1) / gridDim.x;
   const long lo = blockIdx.x * per, hi = min(L, lo + per);
   const float* xr = x + (long)c * L;
@@ -440,6 +446,22 @@ __global__ __launch_bounds__(kNT) void bn_act_apply_stats_kernel(
     if (alpha) z = z > 0.f ? z : al * z;
     yr[i] = z;
   }
+}
+
+// Segmented BatchNorm (one forward over `seg` independent mini-batches stacked along the batch,
+// each normalised by its own statistics): the running statistics take the segments' updates in
+// order, exactly as `seg` separate forwards would (momentum m per update).
+__global__ void bn_running_seq_kernel(int C, int seg, const float* __restrict__ mean, const float* __restrict__ uvar,
+                                      float* running_mean, float* running_var, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float rm = running_mean ? running_mean[c] : 0.f, rv = running_var ? running_var[c] : 0.f;
+  for (int s = 0; s < seg; ++s) {
+    rm = (1.f - momentum) * rm + momentum * mean[c * seg + s];
+    rv = (1.f - momentum) * rv + momentum * uvar[c * seg + s];
+  }
+  if (running_mean) running_mean[c] = rm;
+  if (running_var) running_var[c] = rv;
 }
 
 // Fused second stage of the long-row BatchNorm backward (replaces reduce3 + apply): block (s, c)
@@ -869,27 +891,44 @@ size_t ganamd_rowreduce_workspace(int C, long L) {
   return sizeof(double) * 3 * (size_t)C * splits_for(L) + 2 * sizeof(float) * (size_t)C;
 }
 
+int ganamd_bn_act_fwd_seg(const float* x, int C, long L, int seg, const float* gamma, const float* beta,
+                          const float* alpha, float* running_mean, float* running_var, float momentum, float eps,
+                          float* y, float* save_mean, float* save_invstd, float* seg_uvar, void* workspace,
+                          hipStream_t st) {
+  if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || C <= 0 || L <= 0 || seg < 1 ||
+      L % seg || (seg > 1 && !seg_uvar))
+    return GANAMD_EINVAL;
+  // rows of the segmented problem: (channel, segment), each L / seg long; the parameters of row r
+  // are channel r / seg's, the running statistics are updated per segment in order afterwards
+  const int R = C * seg;
+  const long Lr = L / seg;
+  float* rm = seg > 1 ? nullptr : running_mean;
+  float* rv = seg > 1 ? nullptr : running_var;
+  float* su = seg > 1 ? seg_uvar : nullptr;
+  if (Lr <= kSmallL) {
+    hipLaunchKernelGGL(bn_small_fwd_kernel, dim3((R + 3) / 4), dim3(kNT), 0, st, x, R, (int)Lr, gamma, beta, alpha,
+                       rm, rv, momentum, eps, y, save_mean, save_invstd, seg, su);
+  } else if (Lr <= kMidL) {
+    hipLaunchKernelGGL(bn_mid_fwd_kernel, dim3(R), dim3(kNT), 0, st, x, (int)Lr, gamma, beta, alpha, rm, rv,
+                       momentum, eps, y, save_mean, save_invstd, seg, su);
+  } else {
+    const int S = splits_for(Lr);
+    double* part = static_cast<double*>(workspace);
+    hipLaunchKernelGGL(bn_partial_kernel, dim3(S, R), dim3(kNT), 0, st, x, Lr, S, part);
+    hipLaunchKernelGGL(bn_act_apply_stats_kernel, dim3(S, R), dim3(kNT), 0, st, x, Lr, S, part, rm, rv, momentum, eps,
+                       save_mean, save_invstd, gamma, beta, alpha, y, seg, su);
+  }
+  if (seg > 1 && (running_mean || running_var))
+    hipLaunchKernelGGL(bn_running_seq_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, seg, save_mean, seg_uvar,
+                       running_mean, running_var, momentum);
+  return ok(hipGetLastError());
+}
+
 int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
                       float* save_mean, float* save_invstd, void* workspace, hipStream_t st) {
-  if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || C <= 0 || L <= 0)
-    return GANAMD_EINVAL;
-  if (L <= kSmallL) {
-    hipLaunchKernelGGL(bn_small_fwd_kernel, dim3((C + 3) / 4), dim3(kNT), 0, st, x, C, (int)L, gamma, beta, alpha,
-                       running_mean, running_var, momentum, eps, y, save_mean, save_invstd);
-    return ok(hipGetLastError());
-  }
-  if (L <= kMidL) {
-    hipLaunchKernelGGL(bn_mid_fwd_kernel, dim3(C), dim3(kNT), 0, st, x, (int)L, gamma, beta, alpha, running_mean,
-                       running_var, momentum, eps, y, save_mean, save_invstd);
-    return ok(hipGetLastError());
-  }
-  const int S = splits_for(L);
-  double* part = static_cast<double*>(workspace);
-  hipLaunchKernelGGL(bn_partial_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part);
-  hipLaunchKernelGGL(bn_act_apply_stats_kernel, dim3(S, C), dim3(kNT), 0, st, x, L, S, part, running_mean,
-                     running_var, momentum, eps, save_mean, save_invstd, gamma, beta, alpha, y);
-  return ok(hipGetLastError());
+  return ganamd_bn_act_fwd_seg(x, C, L, 1, gamma, beta, alpha, running_mean, running_var, momentum, eps, y, save_mean,
+                               save_invstd, nullptr, workspace, st);
 }
 
 int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,

@@ -709,5 +709,5 @@ class Generator(nn.Module):
                 for m in bank.mods:
                     m.__dict__["_bank_sd"] = None
         with torch.no_grad():
-            torch._foreach_add_(self._tracked(), 1)
+            torch._foreach_add_(self._tracked(), ops.BN_SEGMENTS[0])   # segmented: one update per segment
         return ops.cnhw_to_nchw(rgb)

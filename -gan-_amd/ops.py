@@ -91,6 +91,17 @@ def math_mode(mode: str):
 PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus", "kernel")
 
 
+@contextlib.contextmanager
+def patch_conv(mask: int = 3):
+    """Route stride-1 convs through the LDS-patch direct kernel (bit 0 forward, bit 1 dgrad)
+    inside the block (ganamd_conv_set_patch; default off, see conv_gemm.hip patch_enabled)."""
+    prev = LIB.ganamd_conv_set_patch(int(mask))
+    try:
+        yield
+    finally:
+        LIB.ganamd_conv_set_patch(prev)
+
+
 def plan_info(geo: "Geo", op: int, scaled: bool = False) -> dict:
     """The block schedule ganamd_conv_fwd / _dgrad launches for this geometry (ganamd_conv_plan_info)."""
     info = (_lib.c_int * 11)()
@@ -624,6 +635,8 @@ def prelu(x, a):
 class BNAct(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, alpha, running_mean, running_var, momentum, eps):
+        if BN_SEGMENTS[0] > 1:
+            raise _lib.GanAmdError("BNAct under bn_segments: use bn_act (the segmented no-grad forward)")
         x = _c(x)
         C, L = _rows(x)
         for t, nm in ((gamma, "gamma"), (beta, "beta"), (alpha, "alpha"), (running_mean, "running_mean"),
@@ -666,11 +679,47 @@ class BNAct(Function):
         return gx, gg, gb, ga, None, None, None, None
 
 
+# Segmented BatchNorm (no-grad forwards only): the batch is BN_SEGMENTS[0] independent mini-batches
+# stacked along it, each normalised by its own statistics (ganamd_bn_act_fwd_seg) -- one generator
+# forward makes the fake batches of all n_critic critic steps (wgangp.Train.generate_fakes).
+BN_SEGMENTS = [1]
+
+
+@contextlib.contextmanager
+def bn_segments(n: int):
+    old = BN_SEGMENTS[0]
+    BN_SEGMENTS[0] = int(n)
+    try:
+        yield
+    finally:
+        BN_SEGMENTS[0] = old
+
+
+def bn_fwd_raw(x, C, L, gamma, beta, alpha, running_mean, running_var, momentum, eps):
+    """Train-mode BatchNorm (+ PReLU) forward of [C][L] rows; honours BN_SEGMENTS.  Returns
+    (y, save_mean, save_invstd) -- per (channel, segment) statistics when segmented."""
+    seg = BN_SEGMENTS[0]
+    if seg > 1 and torch.is_grad_enabled():
+        raise _lib.GanAmdError("segmented BatchNorm is a no-grad forward")
+    if L % seg:
+        raise _lib.GanAmdError(f"BatchNorm: {L} elements per channel do not split into {seg} segments")
+    y = torch.empty_like(x)
+    mean = torch.empty(C * seg, device=x.device, dtype=torch.float32)
+    invstd = torch.empty_like(mean)
+    uvar = torch.empty_like(mean) if seg > 1 else None
+    ws = workspace(LIB.ganamd_rowreduce_workspace(C * seg, L // seg), x.device)
+    check(LIB.ganamd_bn_act_fwd_seg(ptr(x), C, L, seg, ptr(gamma), ptr(beta), ptr(alpha), ptr(running_mean),
+                                    ptr(running_var), float(momentum), float(eps), ptr(y), ptr(mean), ptr(invstd),
+                                    ptr(uvar), ptr(ws), stream()), "bn_act_fwd_seg")
+    return y, mean, invstd
+
+
 def linear_bn_act_ok(x, w) -> bool:
     """Whether ``linear_bn_act`` takes this linear: no autograd, fp32 math (bf16 mode keeps its bf16
-    linears), [Cin, B] with 2 <= B <= 64 and at most 4 M weights (ganamd_linear_bn_act's domain)."""
-    return (not torch.is_grad_enabled() and _MATH[0] == _lib.MATH_F32 and x.dim() == 2 and 2 <= x.shape[1] <= 64
-            and w.shape[0] * w.shape[1] <= (4 << 20))
+    linears), an unsegmented batch, [Cin, B] with 2 <= B <= 64 and at most 4 M weights
+    (ganamd_linear_bn_act's domain)."""
+    return (not torch.is_grad_enabled() and _MATH[0] == _lib.MATH_F32 and BN_SEGMENTS[0] == 1 and x.dim() == 2
+            and 2 <= x.shape[1] <= 64 and w.shape[0] * w.shape[1] <= (4 << 20))
 
 
 def linear_bn_act(x, w, bias, alpha: float, bn, act=None):
@@ -700,6 +749,11 @@ def linear_bn_act(x, w, bias, alpha: float, bn, act=None):
 
 def bn_act(x, bn: torch.nn.modules.batchnorm._BatchNorm, act: torch.nn.PReLU | None = None):
     """Train-mode ``act(bn(x))`` with the module's parameters and running buffers."""
+    if BN_SEGMENTS[0] > 1:
+        x = _c(x)
+        C, L = _rows(x)
+        return bn_fwd_raw(x, C, L, bn.weight, bn.bias, None if act is None else act.weight, bn.running_mean,
+                          bn.running_var, bn.momentum, bn.eps)[0]
     return BNAct.apply(x, bn.weight, bn.bias, None if act is None else act.weight, bn.running_mean, bn.running_var,
                        bn.momentum, bn.eps)
 

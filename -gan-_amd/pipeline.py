@@ -19,6 +19,10 @@ draw order is the same in the replay and in ``eager``, so both draw identical nu
 N > 1: the flat gradient of each optimizer step is all-reduced between the backward graph and the
 optimizer graph (collectives stay outside capture; ``sync``).  ``overlap=False`` captures one graph
 per phase (N = 1: backward + optimizer step in one).
+
+``batch_fakes=True``: the n_critic fake batches come from ONE generator forward over n_critic * B
+samples with segmented BatchNorm (wgangp.Train.generate_fakes) -- wider launches that fill the
+chip better than five B-sample forwards -- replayed before the first critic step.
 """
 from __future__ import annotations
 
@@ -37,8 +41,12 @@ class Iteration:
     ``real_source``: callable returning a synthetic real batch (default: device Philox stream 2 of
     ``tr.rng``, N(0,1) [B,3,64,64], the reference's ImageNet-normalised scale)."""
 
-    def __init__(self, tr, B, n_critic=5, world=1, overlap=True, real_source=None, allreduce=None):
+    def __init__(self, tr, B, n_critic=5, world=1, overlap=True, real_source=None, allreduce=None,
+                 batch_fakes=False):
         self.tr, self.B, self.n_critic, self.world, self.overlap = tr, B, n_critic, world, overlap
+        self.batch_fakes = batch_fakes
+        if batch_fakes and not hasattr(tr, "generate_fakes"):
+            raise ValueError("batch_fakes needs a trainer with generate_fakes (wgangp.Train)")
         self.dev = tr.device
         tr.rng_g                             # create the generator's RNG stream now (snapshot sees it)
         if real_source is None:
@@ -55,12 +63,15 @@ class Iteration:
         critic step on a real batch; n_critic times; then the generator step)."""
         tr, B = self.tr, self.B
         out = []
-        for _ in range(self.n_critic):
-            fake = tr.generate_fake(B)
-            out.append(tr.discriminator_backward(self.real(), B, gen_imgs=fake))
+        fakes = tr.generate_fakes(self.n_critic, B) if self.batch_fakes else None
+        for i in range(self.n_critic):
+            fake = fakes[i] if fakes is not None else tr.generate_fake(B)
+            # detached: a live penalty value would keep its node -- and the critic run with all of
+            # its saved activations -- alive until the iteration returns
+            out.append(tuple(v.detach() for v in tr.discriminator_backward(self.real(), B, gen_imgs=fake)))
             self.allreduce(tr.optimizer_D.flat.grad)
             tr.optimizer_D.step()
-        gen = tr.generator_backward(B)
+        gen = tuple(v.detach() for v in tr.generator_backward(B))
         self.allreduce(tr.optimizer_G.flat.grad)
         tr.optimizer_G.step()
         return out, gen
@@ -87,7 +98,28 @@ class Iteration:
         # peak at once).  Graphs that replay concurrently with them get pools of their own.
         pool = torch.cuda.graph_pool_handle()
         torch.cuda.empty_cache()
-        if self.overlap:
+        if self.batch_fakes:
+            # one generator forward makes all n_critic fake batches; each critic step copies its
+            # batch into the critic graph's fixed input (3 MB, a few microseconds)
+            bufs = {}
+
+            def fakes():
+                bufs["x"] = tr.generate_fakes(self.n_critic, B)
+
+            self.graphs["fake"] = self._capture(fakes, pool)
+            self.graphs["fake"].replay()
+            self.xin = bufs["x"][0].clone()
+            self.bufs = bufs
+            self.graphs["critic"] = self._capture(lambda: tr.discriminator_backward(self.real(), B, gen_imgs=self.xin),
+                                                  pool)
+            if self.world == 1:
+                self.graphs["dstep"] = self._capture(tr.optimizer_D.step, pool)
+                self.graphs["gen"] = self._capture(lambda: (tr.generator_backward(B), tr.optimizer_G.step()), pool)
+            else:
+                self.graphs.update(dstep=self._capture(tr.optimizer_D.step, pool),
+                                   gen=self._capture(lambda: tr.generator_backward(B), pool),
+                                   gstep=self._capture(tr.optimizer_G.step, pool))
+        elif self.overlap:
             bufs = [{}, {}]
 
             def fwd(k):
@@ -126,7 +158,18 @@ class Iteration:
         """Replay one iteration."""
         assert self._captured, "capture() first"
         g, tr = self.graphs, self.tr
-        if self.overlap:
+        if self.batch_fakes:
+            g["fake"].replay()
+            for i in range(self.n_critic):
+                self.xin.copy_(self.bufs["x"][i])
+                g["critic"].replay()
+                self.allreduce(tr.optimizer_D.flat.grad)
+                g["dstep"].replay()
+            g["gen"].replay()
+            if self.world > 1:
+                self.allreduce(tr.optimizer_G.flat.grad)
+                g["gstep"].replay()
+        elif self.overlap:
             cur = torch.cuda.current_stream()
             g["fake"][0].replay()                # G changed in the previous generator step
             for i in range(self.n_critic):
@@ -157,8 +200,12 @@ class Iteration:
     def phase_ms(self):
         """One replay per phase graph, each timed alone (outside the timed region; N = 1)."""
         out = {}
-        items = [("fake", self.graphs["fake"][0]), ("critic", self.graphs["critic"][0]),
-                 ("gen", self.graphs["gen"])] if self.overlap else list(self.graphs.items())
+        if self.batch_fakes:
+            items = [(k, self.graphs[k]) for k in ("fake", "critic", "gen")]
+        elif self.overlap:
+            items = [("fake", self.graphs["fake"][0]), ("critic", self.graphs["critic"][0]), ("gen", self.graphs["gen"])]
+        else:
+            items = list(self.graphs.items())
         for key, g in items:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()

@@ -255,13 +255,8 @@ def grouped_gemm(A, Bm, C, tiles, a_trans=False, b_trans=False, b_square=False, 
 
 
 def _bn_fwd(x, C, L, gamma, beta, alpha, rm, rv):
-    y = torch.empty_like(x)
-    mean = torch.empty(C, device=x.device)
-    invstd = torch.empty_like(mean)
-    ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
-    check(LIB.ganamd_bn_act_fwd(ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(rm), ptr(rv), 0.1, 1e-5,
-                                ptr(y), ptr(mean), ptr(invstd), ptr(ws), stream()), "bn_act_fwd")
-    return y, mean, invstd
+    from .ops import bn_fwd_raw       # segmented statistics when ops.BN_SEGMENTS says so
+    return bn_fwd_raw(x, C, L, gamma, beta, alpha, rm, rv, 0.1, 1e-5)
 
 
 def _bn_bwd(gy, x, C, L, gamma, beta, alpha, mean, invstd, gg, gb, ga):

@@ -141,6 +141,18 @@ class Train(CheckpointMixin):
         with torch.no_grad():
             return self._generate(z)
 
+    def generate_fakes(self, n, b_size):
+        """The fake batches of n critic steps from ONE generator forward over n * b_size samples
+        (wgangp.py:58-59 n times).  G's only cross-sample coupling is train-mode BatchNorm, so the
+        forward runs with segmented BatchNorm (ops.bn_segments): each b_size block is normalised by
+        its own statistics and the running statistics take the n updates in order -- the
+        reference's n separate calls, as one wider launch per layer.  The z and noise values are
+        drawn as one block, so they are other samples of the same distributions than n separate
+        draws would give (the per-stream Philox order is fixed, so a replay draws the same ones)."""
+        z = self.rng_g.randn((n * b_size, self.nz, 1, 1))
+        with torch.no_grad(), ops.bn_segments(n):
+            return self._generate(z).chunk(n)
+
     def discriminator_backward(self, images, b_size, gen_imgs=None):
         """discriminator_trainstep up to (not including) the optimizer step.  ``gen_imgs``: a fake
         batch made beforehand by generate_fake (default: made here, in the reference's order)."""

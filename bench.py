@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one graph per phase, no second-stream fake-batch generation (A/B)")
+    ap.add_argument("--batch-fakes", action="store_true",
+                    help="all n_critic fake batches from one generator forward with segmented BatchNorm")
     return ap.parse_args()
 
 
@@ -161,15 +163,24 @@ PROBES = {
 }
 
 
+def _whole_tile_geo(ops, spec):
+    """The probe's geometry at the spec's batch, or the nearest batch whose plan is ONE launch of
+    whole tiles (no K-split tail + reduce launches), so a launch is the kernel's whole op."""
+    for B in sorted(range(8, 4 * spec["B"] + 1, 8), key=lambda b: (abs(b - spec["B"]), b)):
+        g = ops.conv_geo(B, spec["cin"], spec["h"], spec["h"], spec["cout"], spec["k"], 1, (spec["k"] - 1) // 2)
+        pl = ops.plan_info(g, 0, spec["scaled"])
+        if pl["nfull_t"] == pl["gx"] and pl["S"] == 1:
+            return g, pl
+    raise RuntimeError(f"no whole-tile batch for {spec['shape']}")
+
+
 def probe_kernel(dev, spec, reps=20):
     import gan_amd.ops as ops
-    g = ops.conv_geo(spec["B"], spec["cin"], spec["h"], spec["h"], spec["cout"], spec["k"], 1, (spec["k"] - 1) // 2)
+    g, pl = _whole_tile_geo(ops, spec)
     x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
     w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
     xs = torch.rand(g.Cin, g.B, device=dev) if spec["scaled"] else None
     ys = torch.rand(g.Cout, g.B, device=dev) if spec["scaled"] else None
-    pl = ops.plan_info(g, 0, spec["scaled"])
-    assert pl["nfull_t"] == pl["gx"] and pl["S"] == 1, pl      # one launch, whole tiles (no split-K reduce)
     if pl["kernel"] == 1:                                      # the LDS-patch conv (conv_gemm.hip)
         kernel = f"conv_patch_kernel<{pl['bm']},{g.K},{g.W},{'true' if spec['scaled'] else 'false'}>"
     else:
@@ -200,7 +211,9 @@ def probe_kernel(dev, spec, reps=20):
     us = sum(per) / len(per)
     flop = 2.0 * g.B * g.OH * g.OW * g.Cout * g.Cin * g.K * g.K
     tf = flop / us / 1e6
-    return {"bound": "mfma", "kernel": kernel, "shape": spec["shape"], "blocks": pl["blocks"],
+    shape = spec["shape"] if g.B == spec["B"] else spec["shape"].replace(f"B={spec['B']}", f"B={g.B}") + \
+        f" (B={spec['B']} has a K-split tail; nearest whole-tile batch)"
+    return {"bound": "mfma", "kernel": kernel, "shape": shape, "batch": g.B, "blocks": pl["blocks"],
             "resident_blocks_per_cu": pl["occupancy"],
             "algorithmic_gflop_per_launch": flop / 1e9, "launch_us": us, "launch_us_min": min(per),
             "launch_us_back_to_back": b2b, "achieved": tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -335,7 +348,8 @@ def build(args, dev, rank, world):
         tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=rng)
     B = args.batch
     if args.config != "lazy":
-        return G, D, tr, Iteration(tr, B, N_CRITIC, world, overlap=not args.no_overlap)
+        return G, D, tr, Iteration(tr, B, N_CRITIC, world, overlap=not args.no_overlap,
+                                    batch_fakes=args.batch_fakes)
     data = rng.fork(2)
 
     def real():
@@ -401,7 +415,8 @@ def main():
         it.capture()
         step = it.step
         if rank == 0:
-            print(f"[bench] captured the iteration graphs ({'pipelined' if it.overlap else 'per phase'})",
+            kind = "batched fakes" if it.batch_fakes else ("pipelined" if it.overlap else "per phase")
+            print(f"[bench] captured the iteration graphs ({kind})",
                   file=sys.stderr, flush=True)
     elif args.mode == "graph":
         # one HIP graph per distinct phase (synthetic real batch, z, noise and eps are drawn
@@ -476,9 +491,11 @@ def main():
                 parts[key] = round(e0.elapsed_time(e1), 1)
         print(f"[bench] ms per phase graph: {parts}", file=sys.stderr, flush=True)
         phase_frac = None
-        if headline and pipelined and it.overlap:
-            phase_frac = {k: {"ms": v, "tflops": PHASE_GFLOP_PER_IMAGE[k] * B / v / 1e3,
-                              "frac": PHASE_GFLOP_PER_IMAGE[k] * B / v / 1e3 / FP32_MFMA_PEAK_TFLOPS}
+        if headline and pipelined and (it.overlap or it.batch_fakes):
+            # GFLOP / ms = TFLOP/s; the batched fake phase makes n_critic batches
+            imgs = {k: B * (N_CRITIC if (k == "fake" and it.batch_fakes) else 1) for k in parts}
+            phase_frac = {k: {"ms": v, "tflops": PHASE_GFLOP_PER_IMAGE[k] * imgs[k] / v,
+                              "frac": PHASE_GFLOP_PER_IMAGE[k] * imgs[k] / v / FP32_MFMA_PEAK_TFLOPS}
                           for k, v in parts.items() if k in PHASE_GFLOP_PER_IMAGE}
     probe = census = None
     if "phase_frac" not in locals():

@@ -68,6 +68,10 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
  * GEMM, 1: the LDS-patch conv -- BN is then its 256-pixel region)}.  scaled: whether the
  * x_scale / gy_scale operand will be passed (it selects the kernel instance). */
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info);
+/* Which stride-1 convolutions take the LDS-patch direct kernel: bit 0 forward, bit 1 dgrad
+ * (initially $GANAMD_PATCH, default 0).  mask < 0 only queries.  Returns the previous mask.
+ * Plans are chosen at launch (or graph capture) time. */
+int ganamd_conv_set_patch(int mask);
 
 /* The weight operand of conv_fwd / conv_dgrad in GEMM order (rows padded to the tile grid,
  * channels to whole K-steps, zero filled).  A caller that reuses a weight across calls (the
@@ -140,6 +144,16 @@ size_t ganamd_rowreduce_workspace(int C, long L);
 int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
                       float* save_mean, float* save_invstd, void* workspace, hipStream_t stream);
+/* Segmented form: x holds `seg` independent mini-batches stacked along the batch (each row's L
+ * elements are seg consecutive runs of L / seg), each normalised with its OWN statistics -- the
+ * outputs of seg separate calls, in one launch (the critic steps' fake batches generated in one
+ * generator forward, train/wgangp.py:58-59 x n_critic).  save_mean / save_invstd / seg_uvar:
+ * [C][seg]; running statistics take the seg updates in order.  Workspace:
+ * ganamd_rowreduce_workspace(C * seg, L / seg). */
+int ganamd_bn_act_fwd_seg(const float* x, int C, long L, int seg, const float* gamma, const float* beta,
+                          const float* alpha, float* running_mean, float* running_var, float momentum, float eps,
+                          float* y, float* save_mean, float* save_invstd, float* seg_uvar, void* workspace,
+                          hipStream_t stream);
 
 /* Backward of ganamd_bn_act_fwd: writes gx [C][L]; ggamma, gbeta, galpha ([C]; galpha may be
  * NULL when alpha is NULL) are overwritten, or accumulated into when accumulate = 1 (parameter

@@ -508,15 +508,23 @@ PATCH_CASES = [
     # (conv_patch_kernel: stride 1, "same" padding, 32/64-wide maps, >= 1 round of 1 block per CU)
     (32, 96, 64, 96, 5, 1, True, True),      # G13_5 modulated 5x5 (96 rows: 32x32x2 blocks)
     (32, 48, 64, 48, 3, 1, True, False),     # 48 rows: 16x16x4 blocks
-    (32, 40, 64, 45, 5, 0, False, False),    # ragged rows, channels not a multiple of 16, zero pad
+    (32, 40, 64, 45, 5, 1, False, False),    # ragged rows, channels not a multiple of 16
     (128, 128, 32, 128, 3, 1, False, False), # D9_4 block conv on the critic's 2B batch (two 64-row tiles)
     (16, 108, 64, 108, 5, 1, False, True),   # the ToRGB pre-conv rows (128-row packing, 64-row tiles)
     (128, 64, 32, 96, 5, 1, True, False),    # 32-wide map, 8-row regions
 ]
 
 
+@pytest.fixture
+def patch_on(ops):
+    """The LDS-patch conv is off by default (slower inside the concurrent iteration); these tests
+    switch it on for their duration."""
+    with ops.patch_conv(3):
+        yield
+
+
 @pytest.mark.parametrize("case", PATCH_CASES)
-def test_conv_patch_kernel(ops, case):
+def test_conv_patch_kernel(ops, patch_on, case):
     B, Cin, H, Cout, k, mode, scaled, extra = case
     p = (k - 1) // 2
     geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
@@ -546,6 +554,37 @@ def test_conv_patch_kernel(ops, case):
     got2 = ops._conv_fwd(geo, cn(x), wp, None, f(sx), f(sy), 0.3) if not extra else None
     if got2 is not None:
         assert rel(nc(got2), y) < 1e-5
+
+
+DGRAD_PATCH_CASES = [
+    # B, Cin, H, Cout, k, pad mode, scaled: stride-1 dgrads whose interior takes the LDS-patch conv
+    # (zero-padded, taps reversed) and -- replication padding -- the ring the gather GEMM (s = -2)
+    (32, 96, 64, 96, 5, 1, True),            # G13_5 modulated 5x5 (gy scaled by the demodulation)
+    (32, 48, 64, 40, 3, 1, False),           # 48 rows (16x16x4), K channels not a multiple of 16
+    (128, 128, 32, 128, 3, 1, False),        # D9_4 block conv on the critic's 2B batch
+    (32, 96, 64, 80, 3, 0, False),           # zero padding: no ring
+]
+
+
+@pytest.mark.parametrize("case", DGRAD_PATCH_CASES)
+def test_conv_patch_dgrad(ops, patch_on, case):
+    B, Cin, H, Cout, k, mode, scaled = case
+    p = (k - 1) // 2
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
+    g = torch.Generator().manual_seed(sum(case[:6]) + 7)
+    xm = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64)
+    sy = torch.rand(Cout, B, generator=g, dtype=torch.float64) + 0.5 if scaled else None
+    y = ref_conv(xm, w * 0.3, None, k, 1, p, mode)
+    if scaled:
+        y = y * sy.t()[:, :, None, None]
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    want, = torch.autograd.grad(y, xm, gy)
+    f = (lambda t: None if t is None else t.float().to(DEV))
+    got = ops._conv_dgrad(geo, cn(gy), f(w), f(sy), 0.3)
+    assert rel(nc(got), want) < 1e-5
+    got2 = ops._conv_dgrad(geo, cn(gy), torch.nn.Parameter(f(w)), f(sy), 0.3)   # persistent packed copy
+    assert rel(nc(got2), want) < 1e-5
 
 
 TAIL_CASES = [

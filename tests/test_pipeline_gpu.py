@@ -7,6 +7,9 @@ test_pipelined_iteration_matches_eager  one replay of the captured iteration (fa
     step) and one eager iteration from the same state leave bit-identical parameters, gradients,
     AdamW moments, BatchNorm statistics and RNG offsets; the eager run's draws never share a
     Philox counter.
+test_segmented_batchnorm_op / test_generate_fakes_matches_separate_batches  the batched fake
+    generation (all n_critic fake batches from one generator forward with per-segment BatchNorm
+    statistics) reproduces n separate generator calls.
 test_branch_noise_draws                the first generator forward at a batch size draws its noise
     per StyleConv inside ResnetInit's parallel branch streams: every draw reads the same offset
     with its own draw index (checked against the numpy Philox oracle), and the offset advances
@@ -37,12 +40,12 @@ def _state(tr):
     return [t.detach().clone() for t in training_state(tr)] + [o.clone() for o in tr.rng.state().values()]
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-def test_pipelined_iteration_matches_eager(gan, overlap):
+@pytest.mark.parametrize("mode", ["overlap", "phases", "batched"])
+def test_pipelined_iteration_matches_eager(gan, mode):
     from gan_amd.pipeline import Iteration, restore, snapshot
     G, D = dp_worker.make_models(gan, DEV)
     tr = gan.Train([], DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.DeviceRNG(DEV, 2024))
-    it = Iteration(tr, B, n_critic=5, overlap=overlap)
+    it = Iteration(tr, B, n_critic=5, overlap=mode == "overlap", batch_fakes=mode == "batched")
     it.eager()                      # warm-up: packed weights, noise shapes (bulk draws from here on)
     torch.cuda.synchronize()
     snap = snapshot(tr)
@@ -75,8 +78,100 @@ def test_pipelined_iteration_matches_eager(gan, overlap):
     assert len(set(ctrs)) == len(ctrs), "two draws of one iteration share a Philox counter"
     kinds = {s for s, *_ in draws}
     assert kinds == {0, 1, 2}, kinds            # eps, generator z + noise, real batches
-    # per iteration: 5 eps, 6 z + 6 bulk noise draws, 5 real batches
-    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 12, 5]
+    # per iteration: 5 eps, 6 z + 6 bulk noise draws (batched: 2 + 2), 5 real batches
+    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 4 if mode == "batched" else 12, 5]
+
+
+class _FixedNoise:
+    """A noise source for the generator whose draw i is a fixed [C, n*B, H, W] tensor; a forward
+    over samples [lo, hi) gets that slice of it, so a batched forward and the per-segment forwards
+    see the same noise per sample."""
+
+    def __init__(self, nB):
+        self.nB, self.draws, self.i, self.sl = nB, [], 0, slice(None)
+        self.gen = torch.Generator(device=DEV)
+        self.gen.manual_seed(77)
+
+    def noise(self, shape):
+        Bs, C, H, W = shape
+        if self.i == len(self.draws):
+            self.draws.append(torch.randn((C, self.nB, H, W), device=DEV, generator=self.gen))
+        t = self.draws[self.i][:, self.sl].contiguous()
+        self.i += 1
+        assert t.shape == (C, Bs, H, W)
+        return t
+
+
+def test_segmented_batchnorm_op(gan):
+    """ops.bn_fwd_raw under bn_segments(n) == n separate train-mode BatchNorm+PReLU calls on the
+    segments, bit for bit (same per-row kernel), running statistics included."""
+    from gan_amd import ops
+    torch.manual_seed(3)
+    n, C, Bs, HW = 5, 24, 8, 16 * 16
+    x = torch.randn(C, n * Bs, HW, device=DEV) * 2 + 0.5
+    g, b, a = (torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV), torch.rand(C, device=DEV) * 0.3)
+    rm0, rv0 = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5
+    with torch.no_grad():
+        rm, rv = rm0.clone(), rv0.clone()
+        with ops.bn_segments(n):
+            y, mean, invstd = ops.bn_fwd_raw(x, C, n * Bs * HW, g, b, a, rm, rv, 0.1, 1e-5)
+        rm1, rv1 = rm0.clone(), rv0.clone()
+        for k in range(n):
+            xs = x[:, k * Bs:(k + 1) * Bs].contiguous()
+            ys, ms, iv = ops.bn_fwd_raw(xs, C, Bs * HW, g, b, a, rm1, rv1, 0.1, 1e-5)
+            assert torch.equal(y[:, k * Bs:(k + 1) * Bs], ys), k
+            assert torch.equal(mean.view(C, n)[:, k], ms) and torch.equal(invstd.view(C, n)[:, k], iv)
+    assert torch.equal(rm, rm1) and torch.equal(rv, rv1)
+    with pytest.raises(gan._lib.GanAmdError):
+        with ops.bn_segments(n):
+            ops.bn_fwd_raw(x, C, n * Bs * HW + 1, g, b, a, rm, rv, 0.1, 1e-5)
+
+
+def test_generate_fakes_matches_separate_batches(gan):
+    """Train.generate_fakes(n, B) (one generator forward, segmented BatchNorm) makes the fake
+    batches of n separate generator calls (wgangp.py:58-59 per critic step): same z and noise per
+    sample -> same images (to fp32 summation-order differences of the wider GEMM tilings) and the
+    same BatchNorm running statistics after n updates.  Without segmentation the images differ at
+    O(1e-1) (batch statistics over n*B samples), so the bar has teeth."""
+    from gan_amd import ops
+    n, Bs = 5, 8
+    G, D = dp_worker.make_models(gan, DEV)
+    tr = gan.Train([], DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.DeviceRNG(DEV, 11))
+    z = torch.randn(n * Bs, 256, 1, 1, device=DEV)
+    src = _FixedNoise(n * Bs)
+    G.noise_hub.attach(src)
+    bufs0 = [t.clone() for t in G.buffers()]
+    with torch.no_grad():
+        with ops.bn_segments(n):
+            src.i = 0
+            big = G(z).chunk(n)
+        bufs_big = [t.clone() for t in G.buffers()]
+        for t, v in zip(G.buffers(), bufs0):
+            t.copy_(v)
+        sep = []
+        for k in range(n):
+            src.i, src.sl = 0, slice(k * Bs, (k + 1) * Bs)
+            sep.append(G(z[k * Bs:(k + 1) * Bs]))
+        bufs_sep = [t.clone() for t in G.buffers()]
+        for t, v in zip(G.buffers(), bufs0):
+            t.copy_(v)
+        src.i, src.sl = 0, slice(None)
+        joint = G(z).chunk(n)
+    torch.cuda.synchronize()
+    for k in range(n):
+        d = (big[k] - sep[k]).abs().max().item()
+        assert d < 2e-4, (k, d)
+    worst_joint = max((joint[k] - sep[k]).abs().max().item() for k in range(n))
+    assert worst_joint > 1e-2, worst_joint
+    for a, b in zip(bufs_big, bufs_sep):
+        if a.dtype.is_floating_point:
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+        else:
+            assert torch.equal(a, b)
+    # the trainer's entry: n views of one [n*B, 3, 64, 64] tensor
+    G.noise_hub.attach(tr.rng_g)
+    fakes = tr.generate_fakes(n, Bs)
+    assert len(fakes) == n and all(f.shape == (Bs, 3, 64, 64) for f in fakes)
 
 
 def test_branch_noise_draws(gan):

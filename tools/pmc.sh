@@ -14,9 +14,9 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(float); n = collections.Counter()
 for r in rows:
     k = r["Kernel_Name"]
-    if "gemm" not in k: continue
+    if "gemm" not in k and "patch" not in k: continue
     agg[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
-disp = len({r["Dispatch_Id"] for r in rows if "gemm" in r["Kernel_Name"]})
+disp = len({r["Dispatch_Id"] for r in rows if "gemm" in r["Kernel_Name"] or "patch" in r["Kernel_Name"]})
 print(" ".join(f"{k}={v / max(disp,1):.4g}" for k, v in sorted(agg.items())), f"(per dispatch, {disp} dispatches)")
 PY
 done

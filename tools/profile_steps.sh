@@ -4,7 +4,7 @@
 set -e
 export TMPDIR=/tmp
 TAG=${1:-steps}
-for W in critic generator; do
+for W in ${STEPS:-critic generator}; do
   rm -rf /tmp/prof_$W
   timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/prof_$W -o run --output-format csv -- python3 tools/step_probe.py $W > gpurun_out/${TAG}_${W}_probe.log 2>&1
   T=$(find /tmp/prof_$W -name "*kernel_trace.csv")
