@@ -103,6 +103,10 @@ __global__ __launch_bounds__(kNT) void bn_partial_kernel(const float* __restrict
   }
 }
 
+// running-statistic update r <- (1 - m) r + m v, rounded the same way wherever it is applied (the
+// segmented forward's sequential update must equal the per-call one bit for bit)
+__device__ __forceinline__ float bn_ema(float r, float m, float v) { return __fmaf_rn(1.f - m, r, __fmul_rn(m, v)); }
+
 __device__ __forceinline__ void bn_store_stats(int c, double mean, double m2, long L, float* running_mean,
                                                float* running_var, float momentum, float eps, float* save_mean,
                                                float* save_invstd, float* seg_uvar = nullptr) {
@@ -110,11 +114,8 @@ __device__ __forceinline__ void bn_store_stats(int c, double mean, double m2, lo
   save_mean[c] = (float)mean;
   save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (seg_uvar) seg_uvar[c] = (float)(L > 1 ? m2 / (double)(L - 1) : var);   // segmented: running stats later
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-  if (running_var) {
-    const float unb = (float)(L > 1 ? m2 / (double)(L - 1) : var);
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
-  }
+  if (running_mean) running_mean[c] = bn_ema(running_mean[c], momentum, (float)mean);
+  if (running_var) running_var[c] = bn_ema(running_var[c], momentum, (float)(L > 1 ? m2 / (double)(L - 1) : var));
 }
 
 // Chan merge of the S partials, running-stat update, invstd.
@@ -457,8 +458,8 @@ __global__ void bn_running_seq_kernel(int C, int seg, const float* __restrict__ 
   if (c >= C) return;
   float rm = running_mean ? running_mean[c] : 0.f, rv = running_var ? running_var[c] : 0.f;
   for (int s = 0; s < seg; ++s) {
-    rm = (1.f - momentum) * rm + momentum * mean[c * seg + s];
-    rv = (1.f - momentum) * rv + momentum * uvar[c * seg + s];
+    rm = bn_ema(rm, momentum, mean[c * seg + s]);
+    rv = bn_ema(rv, momentum, uvar[c * seg + s]);
   }
   if (running_mean) running_mean[c] = rm;
   if (running_var) running_var[c] = rv;

@@ -4,12 +4,21 @@ step) as replayed HIP graphs, and its eager twin in the same stream order.
 bench.py times ``Iteration.step`` and tests/test_pipeline_gpu.py checks that one replay equals one
 ``Iteration.eager`` call bit for bit, so the number the bench reports comes from a tested path.
 
-Graph mode, ``overlap=True`` (the headline schedule): the next critic step's
-fake batch (no-grad generator forward, 41 % of a critic step's FLOPs) depends on G's weights only
--- G does not change during the n_critic steps -- so it is replayed on a second HIP stream while
-this step's critic passes, gradient penalty, (N > 1: the RCCL all-reduce) and AdamW run on the
-main stream.  Two copies of the fake-batch graph (own memory pools) double-buffer the batch: the
-side stream writes buffer (i+1) % 2 while the critic reads buffer i % 2.
+Fake batches (no-grad generator forward, 41 % of a critic step's FLOPs) depend on G's weights only,
+and G does not change during the n_critic critic steps, so they need not be made inside each step:
+
+* ``fake_groups`` splits the n_critic fake batches into groups; a group of k is ONE generator
+  forward over k * B samples with segmented BatchNorm (wgangp.Train.generate_fakes: per-B
+  statistics, running statistics updated k times in order) -- wider launches that fill the chip
+  better than k B-sample forwards.  k * B is bounded by the convs' 2^31-byte operand limit
+  (B = 64: k <= 4).
+* ``overlap=True``: group j + 1 is replayed on a second HIP stream while the
+  critic steps of group j (critic passes, gradient penalty, N > 1: the RCCL all-reduce, AdamW) run
+  on the main stream.  Every group has its own graph, memory pool and output buffers.
+
+Each critic step copies its fake batch into the critic graph's fixed input (3 MB).  ``overlap=False``
+with groups of 1 is the reference's order: one graph per phase, the fake batch made inside the
+critic step's graph (N = 1: backward + optimizer step in one graph).
 
 Randomness: every consumer that can run concurrently with another owns its Philox stream
 (rng.py DeviceRNG.fork): the generator's z and noise come from ``tr.rng_g`` (stream 1), the
@@ -17,12 +26,7 @@ critic's eps from ``tr.rng`` (stream 0), the synthetic real batches from stream 
 draw order is the same in the replay and in ``eager``, so both draw identical numbers.
 
 N > 1: the flat gradient of each optimizer step is all-reduced between the backward graph and the
-optimizer graph (collectives stay outside capture; ``sync``).  ``overlap=False`` captures one graph
-per phase (N = 1: backward + optimizer step in one).
-
-``batch_fakes=True``: the n_critic fake batches come from ONE generator forward over n_critic * B
-samples with segmented BatchNorm (wgangp.Train.generate_fakes) -- wider launches that fill the
-chip better than five B-sample forwards -- replayed before the first critic step.
+optimizer graph (collectives stay outside capture).
 """
 from __future__ import annotations
 
@@ -38,15 +42,17 @@ def _sync_none(flat):
 class Iteration:
     """``Iteration(tr, B, n_critic, world)``; ``capture()`` once after an eager warm-up, then
     ``step()`` replays one iteration.  ``eager()`` runs the same iteration without graphs.
+    ``fake_groups``: sizes of the fake-batch groups (default n_critic groups of 1).
     ``real_source``: callable returning a synthetic real batch (default: device Philox stream 2 of
     ``tr.rng``, N(0,1) [B,3,64,64], the reference's ImageNet-normalised scale)."""
 
     def __init__(self, tr, B, n_critic=5, world=1, overlap=True, real_source=None, allreduce=None,
-                 batch_fakes=False):
+                 fake_groups=None):
         self.tr, self.B, self.n_critic, self.world, self.overlap = tr, B, n_critic, world, overlap
-        self.batch_fakes = batch_fakes
-        if batch_fakes and not hasattr(tr, "generate_fakes"):
-            raise ValueError("batch_fakes needs a trainer with generate_fakes (wgangp.Train)")
+        self.groups = [int(k) for k in fake_groups] if fake_groups else [1] * n_critic
+        if sum(self.groups) != n_critic or min(self.groups) < 1:
+            raise ValueError(f"fake_groups {self.groups} do not split {n_critic} critic steps")
+        self.grouped = overlap or max(self.groups) > 1       # fake batches in graphs of their own
         self.dev = tr.device
         tr.rng_g                             # create the generator's RNG stream now (snapshot sees it)
         if real_source is None:
@@ -57,15 +63,21 @@ class Iteration:
         self.graphs = {}
         self._captured = False
 
+    def _fakes(self, k):
+        tr = self.tr
+        return tr.generate_fakes(k, self.B) if hasattr(tr, "generate_fakes") else [tr.generate_fake(self.B)]
+
     # ---- eager ---------------------------------------------------------------------------
     def eager(self):
-        """One iteration without graphs, in the stream order of ``step`` (fake batch, then the
-        critic step on a real batch; n_critic times; then the generator step)."""
+        """One iteration without graphs, in the stream order of ``step`` (fake batches group by
+        group, each critic step on a real batch; n_critic times; then the generator step)."""
         tr, B = self.tr, self.B
         out = []
-        fakes = tr.generate_fakes(self.n_critic, B) if self.batch_fakes else None
-        for i in range(self.n_critic):
-            fake = fakes[i] if fakes is not None else tr.generate_fake(B)
+        fakes, groups = [], list(self.groups)
+        for _ in range(self.n_critic):
+            if not fakes:
+                fakes = list(self._fakes(groups.pop(0)))
+            fake = fakes.pop(0)
             # detached: a live penalty value would keep its node -- and the critic run with all of
             # its saved activations -- alive until the iteration returns
             out.append(tuple(v.detach() for v in tr.discriminator_backward(self.real(), B, gen_imgs=fake)))
@@ -98,114 +110,83 @@ class Iteration:
         # peak at once).  Graphs that replay concurrently with them get pools of their own.
         pool = torch.cuda.graph_pool_handle()
         torch.cuda.empty_cache()
-        if self.batch_fakes:
-            # one generator forward makes all n_critic fake batches; each critic step copies its
-            # batch into the critic graph's fixed input (3 MB, a few microseconds)
-            bufs = {}
+        g = {}
+        if self.grouped:
+            bufs = [{} for _ in self.groups]
 
-            def fakes():
-                bufs["x"] = tr.generate_fakes(self.n_critic, B)
-
-            self.graphs["fake"] = self._capture(fakes, pool)
-            self.graphs["fake"].replay()
-            self.xin = bufs["x"][0].clone()
-            self.bufs = bufs
-            self.graphs["critic"] = self._capture(lambda: tr.discriminator_backward(self.real(), B, gen_imgs=self.xin),
-                                                  pool)
-            if self.world == 1:
-                self.graphs["dstep"] = self._capture(tr.optimizer_D.step, pool)
-                self.graphs["gen"] = self._capture(lambda: (tr.generator_backward(B), tr.optimizer_G.step()), pool)
-            else:
-                self.graphs.update(dstep=self._capture(tr.optimizer_D.step, pool),
-                                   gen=self._capture(lambda: tr.generator_backward(B), pool),
-                                   gstep=self._capture(tr.optimizer_G.step, pool))
-        elif self.overlap:
-            bufs = [{}, {}]
-
-            def fwd(k):
+            def fakes(j):
                 def f():
-                    bufs[k]["x"] = tr.generate_fake(B)
+                    bufs[j]["x"] = self._fakes(self.groups[j])
                 return f
 
-            def crit(k):
-                return lambda: tr.discriminator_backward(self.real(), B, gen_imgs=bufs[k]["x"])
-
-            g_fwd = [None, None]
-            g_crit = [None, None]
-            for k in range(2):
-                g_fwd[k] = self._capture(fwd(k), torch.cuda.graph_pool_handle())
-                g_fwd[k].replay()                # a valid fake batch for the critic capture
-                g_crit[k] = self._capture(crit(k), pool)
-            self.graphs = {"fake": g_fwd, "critic": g_crit,
-                           "dstep": self._capture(tr.optimizer_D.step, pool),
-                           "gen": self._capture(lambda: tr.generator_backward(B), pool),
-                           "gstep": self._capture(tr.optimizer_G.step, pool)}
-            self.side = torch.cuda.Stream()
+            g["fake"] = [self._capture(fakes(j), torch.cuda.graph_pool_handle() if self.overlap else pool)
+                         for j in range(len(self.groups))]
+            g["fake"][0].replay()                # a valid fake batch for the critic capture
+            self.xin = bufs[0]["x"][0].clone()
             self.bufs = bufs
+            g["critic"] = self._capture(lambda: tr.discriminator_backward(self.real(), B, gen_imgs=self.xin), pool)
+            g["dstep"] = self._capture(tr.optimizer_D.step, pool)
+            self.side = torch.cuda.Stream()
         else:
             crit = lambda: tr.discriminator_backward(self.real(), B)     # noqa: E731
-            gen = lambda: tr.generator_backward(B)                      # noqa: E731
             if self.world == 1:
-                self.graphs = {"critic": self._capture(lambda: (crit(), tr.optimizer_D.step()), pool),
-                               "gen": self._capture(lambda: (gen(), tr.optimizer_G.step()), pool)}
+                g["critic"] = self._capture(lambda: (crit(), tr.optimizer_D.step()), pool)
             else:
-                self.graphs = {"critic": self._capture(crit, pool), "dstep": self._capture(tr.optimizer_D.step, pool),
-                               "gen": self._capture(gen, pool), "gstep": self._capture(tr.optimizer_G.step, pool)}
+                g["critic"] = self._capture(crit, pool)
+                g["dstep"] = self._capture(tr.optimizer_D.step, pool)
+        gen = lambda: tr.generator_backward(B)                          # noqa: E731
+        if self.world == 1:
+            g["gen"] = self._capture(lambda: (gen(), tr.optimizer_G.step()), pool)
+        else:
+            g["gen"] = self._capture(gen, pool)
+            g["gstep"] = self._capture(tr.optimizer_G.step, pool)
+        self.graphs = g
         torch.cuda.synchronize()
         self._captured = True
+
+    def _critic_step(self):
+        g = self.graphs
+        g["critic"].replay()
+        if "dstep" in g:
+            self.allreduce(self.tr.optimizer_D.flat.grad)
+            g["dstep"].replay()
 
     def step(self):
         """Replay one iteration."""
         assert self._captured, "capture() first"
-        g, tr = self.graphs, self.tr
-        if self.batch_fakes:
-            g["fake"].replay()
-            for i in range(self.n_critic):
-                self.xin.copy_(self.bufs["x"][i])
-                g["critic"].replay()
-                self.allreduce(tr.optimizer_D.flat.grad)
-                g["dstep"].replay()
-            g["gen"].replay()
-            if self.world > 1:
-                self.allreduce(tr.optimizer_G.flat.grad)
-                g["gstep"].replay()
-        elif self.overlap:
+        g = self.graphs
+        if self.grouped:
             cur = torch.cuda.current_stream()
             g["fake"][0].replay()                # G changed in the previous generator step
-            for i in range(self.n_critic):
-                if i + 1 < self.n_critic:        # the next step's fake batch, concurrently
-                    self.side.wait_stream(cur)   # (its buffer was last read two steps ago)
+            n = len(self.groups)
+            for j, k in enumerate(self.groups):
+                ahead = j + 1 < n
+                if ahead and self.overlap:       # the next group's fake batches, concurrently
+                    self.side.wait_stream(cur)
                     with torch.cuda.stream(self.side):
-                        g["fake"][(i + 1) % 2].replay()
-                g["critic"][i % 2].replay()
-                self.allreduce(tr.optimizer_D.flat.grad)
-                g["dstep"].replay()
-                cur.wait_stream(self.side)
-            g["gen"].replay()
-            self.allreduce(tr.optimizer_G.flat.grad)
-            g["gstep"].replay()
-        elif self.world == 1:
-            for _ in range(self.n_critic):
-                g["critic"].replay()
-            g["gen"].replay()
+                        g["fake"][j + 1].replay()
+                for q in range(k):
+                    with torch.no_grad():        # (the critic step marks its fake batch requires_grad)
+                        self.xin.copy_(self.bufs[j]["x"][q])
+                    self._critic_step()
+                if ahead:
+                    if self.overlap:
+                        cur.wait_stream(self.side)
+                    else:
+                        g["fake"][j + 1].replay()
         else:
             for _ in range(self.n_critic):
-                g["critic"].replay()
-                self.allreduce(tr.optimizer_D.flat.grad)
-                g["dstep"].replay()
-            g["gen"].replay()
-            self.allreduce(tr.optimizer_G.flat.grad)
+                self._critic_step()
+        g["gen"].replay()
+        if "gstep" in g:
+            self.allreduce(self.tr.optimizer_G.flat.grad)
             g["gstep"].replay()
 
     def phase_ms(self):
-        """One replay per phase graph, each timed alone (outside the timed region; N = 1)."""
+        """One replay per phase graph, each timed alone (outside the timed region; N = 1).  The
+        fake phase is the first group's graph (``groups[0]`` batches)."""
         out = {}
-        if self.batch_fakes:
-            items = [(k, self.graphs[k]) for k in ("fake", "critic", "gen")]
-        elif self.overlap:
-            items = [("fake", self.graphs["fake"][0]), ("critic", self.graphs["critic"][0]), ("gen", self.graphs["gen"])]
-        else:
-            items = list(self.graphs.items())
+        items = [(k, v[0] if isinstance(v, list) else v) for k, v in self.graphs.items()]
         for key, g in items:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()

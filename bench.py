@@ -57,11 +57,35 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the post-run breakdown and roofline probe (clean traces of the timed region)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (functional test of N>1 on one GPU)")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="one graph per phase, no second-stream fake-batch generation (A/B)")
-    ap.add_argument("--batch-fakes", action="store_true",
-                    help="all n_critic fake batches from one generator forward with segmented BatchNorm")
+    ap.add_argument("--overlap", choices=["on", "off"], default=None,
+                    help="make the next fake-batch group on a second stream during the current group's critic "
+                         "steps (default: the headline schedule's FAKE_OVERLAP; groups of 1 without overlap = "
+                         "one graph per phase, the reference's order)")
+    ap.add_argument("--fake-groups", default=None, metavar="K,K,...",
+                    help="fake-batch groups of the n_critic steps, each one generator forward with segmented "
+                         "BatchNorm (default: the headline schedule FAKE_GROUPS)")
     return ap.parse_args()
+
+
+# Fake batches of the n_critic critic steps (pipeline.Iteration): groups made by one segmented-
+# BatchNorm generator forward each, optionally the next group on a second stream during the current
+# group's critic steps.  k * B must keep every conv operand under 2^31 bytes (B = 64: k <= 4).
+# Measured at B = 64 (profiles/r03_ab_fake_groups.txt): (1,1,1,1,1) overlapped 41.3 img/s, (4,1)
+# overlapped 42.7, (4,1) serial 42.8 -- the wide forward fills the chip on its own.
+FAKE_GROUPS, FAKE_OVERLAP = (4, 1), False
+
+
+def fake_schedule(args, B):
+    """(overlap, real_source, allreduce, fake_groups) arguments of pipeline.Iteration."""
+    if args.fake_groups:
+        groups = [int(k) for k in args.fake_groups.split(",")]
+    elif args.config == "wgangp" and B <= 64:
+        groups = list(FAKE_GROUPS)
+    else:
+        groups = [1] * N_CRITIC
+    default = FAKE_OVERLAP if max(groups) > 1 else True
+    overlap = default if args.overlap is None else args.overlap == "on"
+    return overlap, None, None, groups
 
 
 def _free_port():
@@ -348,8 +372,7 @@ def build(args, dev, rank, world):
         tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=rng)
     B = args.batch
     if args.config != "lazy":
-        return G, D, tr, Iteration(tr, B, N_CRITIC, world, overlap=not args.no_overlap,
-                                    batch_fakes=args.batch_fakes)
+        return G, D, tr, Iteration(tr, B, N_CRITIC, world, *fake_schedule(args, B))
     data = rng.fork(2)
 
     def real():
@@ -415,7 +438,7 @@ def main():
         it.capture()
         step = it.step
         if rank == 0:
-            kind = "batched fakes" if it.batch_fakes else ("pipelined" if it.overlap else "per phase")
+            kind = f"fake groups {it.groups}, {'overlapped' if it.overlap else 'serial'}"
             print(f"[bench] captured the iteration graphs ({kind})",
                   file=sys.stderr, flush=True)
     elif args.mode == "graph":
@@ -491,9 +514,9 @@ def main():
                 parts[key] = round(e0.elapsed_time(e1), 1)
         print(f"[bench] ms per phase graph: {parts}", file=sys.stderr, flush=True)
         phase_frac = None
-        if headline and pipelined and (it.overlap or it.batch_fakes):
+        if headline and pipelined and it.grouped:
             # GFLOP / ms = TFLOP/s; the batched fake phase makes n_critic batches
-            imgs = {k: B * (N_CRITIC if (k == "fake" and it.batch_fakes) else 1) for k in parts}
+            imgs = {k: B * (it.groups[0] if k == "fake" else 1) for k in parts}
             phase_frac = {k: {"ms": v, "tflops": PHASE_GFLOP_PER_IMAGE[k] * imgs[k] / v,
                               "frac": PHASE_GFLOP_PER_IMAGE[k] * imgs[k] / v / FP32_MFMA_PEAK_TFLOPS}
                           for k, v in parts.items() if k in PHASE_GFLOP_PER_IMAGE}
@@ -529,6 +552,9 @@ def main():
         }
         if headline:
             out["config"]["n_critic"] = N_CRITIC
+            if pipelined:
+                out["config"]["fake_groups"] = it.groups
+                out["config"]["fake_overlap"] = it.overlap
             achieved = ALGO_GFLOP_PER_IMAGE * 1e9 * B / t_iter / 1e12      # per GPU
             out["roofline"] = dict(probe or {}, **{
                 # whole iteration: algorithmic FLOPs / iteration time, per GPU

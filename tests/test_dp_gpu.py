@@ -7,8 +7,9 @@ one after another on the same weights and replayed random streams, their gradien
 by hand, and the critic update is applied from that mean.  The all-reduced gradients and the
 updated critic must match at 1e-5 (gloo sums the fp32 buffers on the host: one rounding).
 
-test_dp_graph_iteration_matches_shard_mean: the bench's N > 1 GRAPH-mode path (pipelined
-iteration, side-stream fake batches, all-reduce between captured graphs) on two ranks equals, after
+test_dp_graph_iteration_matches_shard_mean: the bench's N > 1 GRAPH-mode path (pipeline.Iteration
+with the bench's fake-batch groups 4 + 1 from segmented-BatchNorm generator forwards, all-reduce
+between captured graphs) on two ranks equals, after
 one full iteration (5 critic steps + generator step), the same iteration run here eagerly with the
 two shards one after another and their gradients averaged by hand before every optimizer step.
 
@@ -101,19 +102,22 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path):
     G, D = dp_worker.make_models(gan_amd, dev)
     tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev, 1))
     g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
-    with torch.no_grad():
-        tr.generate_fake(B)        # the workers' warm-up recorded the noise shapes: bulk draws from here
+    for k in set(dp_worker.GRAPH_FAKE_GROUPS):
+        tr.generate_fakes(k, B)    # the workers' warm-up recorded the noise shapes: bulk draws from here
     rngs = [gan_amd.DeviceRNG(dev, dp_worker.graph_seed(r)) for r in range(2)]
+    fakes = []                     # each rank's fake batches, group by group (G is fixed until the G step)
+    for rng in rngs:
+        tr.rng = rng
+        fakes.append([f for k in dp_worker.GRAPH_FAKE_GROUPS for f in tr.generate_fakes(k, B)])
 
     def mean_into(flat_grad, gs):
         flat_grad.copy_(gs[0] + gs[1]).mul_(0.5)          # gloo: SUM, then * 1/N (dist.allreduce_mean_)
 
-    for _ in range(5):
+    for i in range(5):
         gs = []
-        for rng in rngs:
+        for r, rng in enumerate(rngs):
             tr.rng = rng
-            fake = tr.generate_fake(B)
-            tr.discriminator_backward(rng.fork(2).randn((B, 3, 64, 64)), B, gen_imgs=fake)
+            tr.discriminator_backward(rng.fork(2).randn((B, 3, 64, 64)), B, gen_imgs=fakes[r][i])
             gs.append(tr.optimizer_D.flat.grad.detach().clone())
         assert _rel(gs[0].cpu(), gs[1].cpu()) > 1e-2       # the shards really differ
         mean_into(tr.optimizer_D.flat.grad, gs)

@@ -45,7 +45,7 @@ def test_pipelined_iteration_matches_eager(gan, mode):
     from gan_amd.pipeline import Iteration, restore, snapshot
     G, D = dp_worker.make_models(gan, DEV)
     tr = gan.Train([], DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.DeviceRNG(DEV, 2024))
-    it = Iteration(tr, B, n_critic=5, overlap=mode == "overlap", batch_fakes=mode == "batched")
+    it = Iteration(tr, B, n_critic=5, overlap=mode != "phases", fake_groups=[1, 3, 1] if mode == "batched" else None)
     it.eager()                      # warm-up: packed weights, noise shapes (bulk draws from here on)
     torch.cuda.synchronize()
     snap = snapshot(tr)
@@ -78,8 +78,8 @@ def test_pipelined_iteration_matches_eager(gan, mode):
     assert len(set(ctrs)) == len(ctrs), "two draws of one iteration share a Philox counter"
     kinds = {s for s, *_ in draws}
     assert kinds == {0, 1, 2}, kinds            # eps, generator z + noise, real batches
-    # per iteration: 5 eps, 6 z + 6 bulk noise draws (batched: 2 + 2), 5 real batches
-    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 4 if mode == "batched" else 12, 5]
+    # per iteration: 5 eps, 6 z + 6 bulk noise draws (batched in groups 1, 3, 1: 4 + 4), 5 real batches
+    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 8 if mode == "batched" else 12, 5]
 
 
 class _FixedNoise:

@@ -13,6 +13,9 @@ run() {
   python3 -c "import json; d=json.loads(open('gpurun_out/${TAG}_b.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])" >> $OUT
 }
 run python3 bench.py
-run python3 bench.py --batch-fakes
-run env GANAMD_PATCH=3 python3 bench.py --batch-fakes
+run python3 bench.py --fake-groups 1,4
+run python3 bench.py --fake-groups 1,2,2
+run python3 bench.py --fake-groups 4,1
+run python3 bench.py --fake-groups 4,1 --overlap off
+run python3 bench.py --fake-groups 2,3
 cat $OUT
