@@ -277,6 +277,62 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 // lane's 8 k-values are rounded to bf16 (RNE) and ONE v_mfma_f32_32x32x16_bf16 replaces the 8
 // f32 steps -- its operand map is exactly this one (lane (r, h) holds A[r][8h + j] and
 // B[8h + j][r], j = 0..7) and its C/D map that of 32x32x2 f32, so nothing else changes.
+// ---- fp32 products on the bf16 matrix cores (GANAMD_SPLIT6) ----------------------------------
+// x = h + m + l with h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (RNE; the two differences
+// are exact in fp32), so x is kept to 24 significant bits.  x * y is then the six bf16 products
+// with at least one high part -- hh + (hm + mh) + (hl + lh + mm) -- exact in the MFMA; the three
+// dropped ones (ml, lm, ll) are below 2^-24 |x y|, fp32's own rounding.  Six
+// v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) replace eight v_mfma_f32_32x32x2_f32 (8 x 64).
+#ifndef GANAMD_SPLIT6
+#define GANAMD_SPLIT6 1
+#endif
+#ifndef GANAMD_SPLIT6_16   // the 16x16 blocks too (v_mfma_f32_16x16x16_bf16, half the bf16 rate)
+#define GANAMD_SPLIT6_16 1
+#endif
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+template <int N, class V>
+__device__ __forceinline__ void split3(const float* x, V& h, V& m, V& l) {
+  float r[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    h[e] = (__bf16)x[e];
+    r[e] = x[e] - (float)h[e];
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    m[e] = (__bf16)r[e];
+    r[e] -= (float)m[e];
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) l[e] = (__bf16)r[e];
+}
+
+__device__ __forceinline__ f32x16 mfma6_32(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                           const bf16x8& bm, const bf16x8& bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 mfma6_16(const bf16x4& ah, const bf16x4& am, const bf16x4& al, const bf16x4& bh,
+                                          const bf16x4& bm, const bf16x4& bl, f32x4 acc) {
+#define GANAMD_M16(x, y) __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, x), \
+                                                                   __builtin_bit_cast(s16x4, y), acc, 0, 0, 0)
+  acc = GANAMD_M16(al, bh);
+  acc = GANAMD_M16(ah, bl);
+  acc = GANAMD_M16(am, bm);
+  acc = GANAMD_M16(am, bh);
+  acc = GANAMD_M16(ah, bm);
+  acc = GANAMD_M16(ah, bh);
+#undef GANAMD_M16
+  return acc;
+}
+
 template <class C, int LD = LDK, bool BF16 = false>
 __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
                                           typename C::acc_t (&acc)[C::TM][C::TN], int lane, int wm, int wn, int k0) {
@@ -296,6 +352,18 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
       const float* src = Bs + ((wn * C::TN + j) * 16 + r) * LD + k0 + 4 * q;
       const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
       b[j][0] = t0[0]; b[j][1] = t0[1]; b[j][2] = t1[0]; b[j][3] = t1[1];
+    }
+    if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT6_16) {   // 16x16x16 bf16: lane (r, q) holds A[r][4q..4q+3] -- this map
+      bf16x4 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) split3<4>(a[i], ah[i], am[i], al[i]);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) split3<4>(b[j], bh[j], bm[j], bl[j]);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_16(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
+      return;
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -327,6 +395,18 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
 #pragma unroll
       for (int j = 0; j < C::TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    return;
+  }
+  if constexpr (GANAMD_SPLIT6) {
+    bf16x8 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i) split3<8>(a[i], ah[i], am[i], al[i]);
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) split3<8>(b[j], bh[j], bm[j], bl[j]);
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_32(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
     return;
   }
 #ifdef GANAMD_SETPRIO
@@ -649,6 +729,52 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
   }
 }
 
+// Epilogue of the conv GEMM bodies: C/D map of the block MFMA (mfma_row).  Split-K blocks store
+// raw partial tiles to their slab; the reduce kernel applies the rest.
+template <class C, int MODE>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const typename C::acc_t (&acc)[C::TM][C::TN], int n0,
+                                              int m0, int split, int lane, int wm, int wn) {
+  const Gather& g = p.g;
+  const bool finish = split < 0 || p.S == 1;
+  float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
+  const long ldo = finish ? p.ldy : p.tail_cols;
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j) {
+    const int n = n0 + (wn * C::TN + j) * C::MB + (lane & (C::MB - 1));
+    if (n >= p.N) continue;
+    const int b = (finish && p.oscale) ? n / p.ohw : 0;
+    float* obase = out;
+    long old = ldo, col = n;
+    if (finish) {
+      if constexpr (MODE == kPhase) col = out_col(p.om, n);
+      if constexpr (MODE == kTransposed) {
+        if (p.om.s == -2) {
+          obase = p.om.ring;
+          old = p.om.ldr;
+        } else if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) {
+          continue;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < C::NR; ++r) {
+        const int m = m0 + (wm * C::TM + i) * C::MB + mfma_row<C::MB>(lane, r);
+        if (m >= p.M) continue;
+        float v = p.alpha * acc[i][j][r];
+        if (finish) {
+          if (p.oscale) v *= p.oscale[m * g.B + b];
+          if (p.bias) v += p.bias[m];
+          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
+          if (p.act) v = v > 0.f ? v : p.act[m] * v;
+        }
+        obase[(long)m * old + col] = v;
+      }
+    }
+  }
+}
+
 #ifndef GANAMD_CONV_WPE
 #define GANAMD_CONV_WPE 1
 #endif
@@ -658,11 +784,223 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
 __device__ __forceinline__ void conv_body_f32(const ConvArgs& p);
 
+
+// ---- fp32 GEMM body with split operands in LDS (GANAMD_SPLIT_LDS) ----------------------------
+// conv_body_f32's block schedule and gather, but each operand element is split ONCE -- by the
+// thread that stores it to LDS -- into three bf16 planes (h, m, l: split3); the waves read bf16
+// fragments and issue the six split products per 16 k on the bf16 matrix cores (mfma6_32 /
+// mfma6_16) instead of splitting every fragment they read.  K-step 16; 48-byte plane rows (16 k
+// + 8 pad): the fragment reads (ds_read_b128 / _b64) and the 8-k slot stores (ds_write_b128) are
+// conflict-free (MI355X_MICROARCH.md "LDS" lane groups).
+#ifndef GANAMD_SPLIT_LDS
+#define GANAMD_SPLIT_LDS 1
+#endif
+constexpr int LDH = BK + 8;
+
+template <class C, int PSA, int PSB>
+__device__ __forceinline__ void mfma_tile_x3(const unsigned short* __restrict__ As, const unsigned short* __restrict__ Bs,
+                                             typename C::acc_t (&acc)[C::TM][C::TN], int lane, int wm, int wn) {
+  if constexpr (C::MB == 16) {   // 16x16x16 bf16: lane (r, q) holds k = 4q .. 4q+3 of row r
+    const int r = lane & 15, q = lane >> 4;
+    bf16x4 a[C::TM][3], b[C::TN][3];
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = *reinterpret_cast<const bf16x4*>(&As[pl * PSA + ((wm * C::TM + i) * 16 + r) * LDH + 4 * q]);
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[j][pl] = *reinterpret_cast<const bf16x4*>(&Bs[pl * PSB + ((wn * C::TN + j) * 16 + r) * LDH + 4 * q]);
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = mfma6_16(a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2], acc[i][j]);
+  } else {                       // 32x32x16 bf16: lane (r, h) holds k = 8h .. 8h+7 of row r
+    const int r = lane & 31, h = lane >> 5;
+    bf16x8 a[C::TM][3], b[C::TN][3];
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl * PSA + ((wm * C::TM + i) * 32 + r) * LDH + 8 * h]);
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[j][pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl * PSB + ((wn * C::TN + j) * 32 + r) * LDH + 8 * h]);
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = mfma6_32(a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2], acc[i][j]);
+  }
+}
+
+// the three bf16 planes of 8 consecutive fp32 values to plane rows at `d` (plane stride PS)
+template <int PS>
+__device__ __forceinline__ void store_split8(unsigned short* d, const float* v) {
+  bf16x8 h, m, l;
+  split3<8>(v, h, m, l);
+  *reinterpret_cast<bf16x8*>(d) = h;
+  *reinterpret_cast<bf16x8*>(d + PS) = m;
+  *reinterpret_cast<bf16x8*>(d + 2 * PS) = l;
+}
+
+template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
+__device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
+  using C = TileCfg<BM, BN, WGM, WGN>;
+  constexpr int SPR = BK / 8;                          // 8-k A slots per row and K-step
+  constexpr int SA = BM * SPR;
+  constexpr int EA = (SA + kThreads - 1) / kThreads;   // slots per thread
+  constexpr int KPT = BK * BN / kThreads;              // B k-values per thread
+  static_assert(KPT % 8 == 0 && BK % KPT == 0, "B mapping");
+  constexpr int PSA = BM * LDH, PSB = BN * LDH;
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][3 * PSA];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * PSB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int nct = p.Ckp / BK;
+  const int kt_total = nct * p.T;
+  int tx, ty, kt0, kt1, split = -1;
+  {
+    const int bid = blockIdx.x;
+    if (bid < p.full_blocks) {
+      ty = bid % p.gy;
+      tx = bid / p.gy;
+      kt0 = 0;
+      kt1 = kt_total;
+    } else {
+      const int t = bid - p.full_blocks;
+      const int r = t / p.S;
+      split = t - r * p.S;
+      ty = r % p.gy;
+      tx = p.nfull_t + r / p.gy;
+      kt0 = split * p.kt_per_split;
+      kt1 = min(kt_total, kt0 + p.kt_per_split);
+    }
+  }
+  const int n0 = tx * BN, m0 = ty * BM;
+
+  const int Krow = p.T * p.Ckp;
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  int a_off[EA];
+#pragma unroll
+  for (int e = 0; e < EA; ++e) {
+    const int slot = tid + e * kThreads;
+    a_off[e] = 4 * ((m0 + slot / SPR) * Krow + 8 * (slot % SPR));
+  }
+
+  const int b_n = tid % BN, b_kg = tid / BN;
+  const Gather& g = p.g;
+  const int gn = n0 + b_n;
+  const bool n_ok = gn < p.N;
+  int bb = 0, oh = 0, ow = 0;
+  if (n_ok) {
+    bb = gn / p.ohw;
+    const int rr = gn - bb * p.ohw;
+    if (MODE == kTransposed && p.om.s == -2) {
+      ring_coord(rr, p.om.qh, p.om.qw, p.om.OW, p.om.OWp, oh, ow);
+    } else {
+      oh = rr / g.OW;
+      ow = rr - oh * g.OW;
+    }
+  }
+  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
+  const int img = bb * g.H * g.W;
+  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
+
+  struct Stage {
+    f32x4 ra[EA][2];
+    float rb[KPT], rs[KPT];
+  };
+  int cc = kt0 / p.T;
+  int kh, kw;
+  {
+    const int t = kt0 - cc * p.T;
+    kh = t / g.KW;
+    kw = t - kh * g.KW;
+  }
+  auto tap = [&]() { return n_ok ? tap_offset<MODE>(g, oh, ow, kh, kw) : -1; };
+  int sp = tap();
+
+  auto gload = [&](int kt, Stage& S) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e)
+      if (tid + e * kThreads < SA) {
+        S.ra[e][0] = bload4(rw, a_off[e] + kt * (BK * 4));
+        S.ra[e][1] = bload4(rw, a_off[e] + kt * (BK * 4) + 16);
+      }
+    const int c = cc * BK + b_kg * KPT;
+    const unsigned base = sp >= 0 ? 4u * (unsigned)(img + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
+    const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + bb) : (unsigned)kOOB;
+#pragma unroll
+    for (int e = 0; e < KPT; ++e) {
+      S.rb[e] = bload(rx, (int)(base + (unsigned)e * cs4));
+      if (BSCALE) S.rs[e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
+    }
+    if (++kw == g.KW) {
+      kw = 0;
+      if (++kh * g.KW >= p.T) {
+        kh = 0;
+        ++cc;
+      }
+    }
+    sp = tap();
+  };
+  auto sstore = [&](int buf, const Stage& S) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int slot = tid + e * kThreads;
+      if (slot < SA) {
+        const float v[8] = {S.ra[e][0][0], S.ra[e][0][1], S.ra[e][0][2], S.ra[e][0][3],
+                            S.ra[e][1][0], S.ra[e][1][1], S.ra[e][1][2], S.ra[e][1][3]};
+        store_split8<PSA>(&As[buf][(slot / SPR) * LDH + 8 * (slot % SPR)], v);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < KPT; e += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = BSCALE ? S.rb[e + q] * S.rs[e + q] : S.rb[e + q];
+      store_split8<PSB>(&Bs[buf][b_n * LDH + b_kg * KPT + e], v);
+    }
+  };
+
+  typename C::acc_t acc[C::TM][C::TN];
+  zero_acc<C>(acc);
+
+  Stage s0, s1;
+  gload(kt0, s0);
+  sstore(0, s0);
+  if (kt0 + 1 < kt1) gload(kt0 + 1, s1);
+  __syncthreads();
+  int kt = kt0;
+  for (; kt + 1 < kt1; kt += 2) {
+    if (kt + 2 < kt1) gload(kt + 2, s0);
+    mfma_tile_x3<C, PSA, PSB>(As[0], Bs[0], acc, lane, wm, wn);
+    sstore(1, s1);
+    __syncthreads();
+    if (kt + 3 < kt1) gload(kt + 3, s1);
+    mfma_tile_x3<C, PSA, PSB>(As[1], Bs[1], acc, lane, wm, wn);
+    if (kt + 2 < kt1) sstore(0, s0);
+    __syncthreads();
+  }
+  if (kt < kt1) mfma_tile_x3<C, PSA, PSB>(As[0], Bs[0], acc, lane, wm, wn);
+  conv_epilogue<C, MODE>(p, acc, n0, m0, split, lane, wm, wn);
+}
+
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD_CONV_WPE)))
 void conv_gemm_kernel(ConvArgs p) {
   if constexpr (BF16) {
     conv_body_bf16<BM, BN, WGM, WGN, MODE, BSCALE>(p);
+  } else if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT_LDS) {
+    conv_body_x3<BM, BN, WGM, WGN, MODE, BSCALE>(p);
   } else {
     conv_body_f32<BM, BN, WGM, WGN, MODE, BSCALE>(p);
   }
@@ -851,46 +1189,7 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
   }
 #endif
 
-  // epilogue: C/D map of the block MFMA (mfma_row).  Split-K blocks store raw partial tiles to
-  // their slab; the reduce kernel applies the rest.
-  const bool finish = split < 0 || p.S == 1;
-  float* out = finish ? p.y : p.slab + (long)split * p.M * p.tail_cols - p.tail_n0;
-  const long ldo = finish ? p.ldy : p.tail_cols;
-#pragma unroll
-  for (int j = 0; j < C::TN; ++j) {
-    const int n = n0 + (wn * C::TN + j) * C::MB + (lane & (C::MB - 1));
-    if (n >= p.N) continue;
-    const int b = (finish && p.oscale) ? n / p.ohw : 0;
-    float* obase = out;
-    long old = ldo, col = n;
-    if (finish) {
-      if constexpr (MODE == kPhase) col = out_col(p.om, n);
-      if constexpr (MODE == kTransposed) {
-        if (p.om.s == -2) {
-          obase = p.om.ring;
-          old = p.om.ldr;
-        } else if (p.om.s < 0 && !frame_target(p.om, p.y, p.ldy, n, obase, old, col)) {
-          continue;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < C::TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < C::NR; ++r) {
-        const int m = m0 + (wm * C::TM + i) * C::MB + mfma_row<C::MB>(lane, r);
-        if (m >= p.M) continue;
-        float v = p.alpha * acc[i][j][r];
-        if (finish) {
-          if (p.oscale) v *= p.oscale[m * g.B + b];
-          if (p.bias) v += p.bias[m];
-          if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
-          if (p.act) v = v > 0.f ? v : p.act[m] * v;
-        }
-        obase[(long)m * old + col] = v;
-      }
-    }
-  }
+  conv_epilogue<C, MODE>(p, acc, n0, m0, split, lane, wm, wn);
 }
 
 // ---- LDS-patch conv: stride 1, "same" padding, K x K taps (K = 3, 5), maps 32 / 64 wide ----------
@@ -1581,7 +1880,7 @@ constexpr double reduce_launch_us() { return 3.0; }
 // x CUs) of ceil(kt_total/s) K-steps; splitting adds the slab round trip and a reduce launch.
 // (A CU-level "fluid" model -- one block alone runs at the CU's full rate -- was measured to
 // under-split the big-K wgrads 1.4-2x: a lone block of 4 waves does not fill its CU.)
-constexpr double kBlockTflops = 110.0;   // measured sustained fp32 MFMA rate of the GEMM kernels
+constexpr double kBlockTflops = 130.0;   // measured sustained fp32 rate of the GEMM kernels (split6 products)
 Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_elems, int occ, int max_splits,
                 int min_k) {
   const int slots = occ * kCUs;
@@ -1702,7 +2001,7 @@ double list_makespan(long F, double L, long R, double d, long slots) {
   }
 }
 
-constexpr double kSustainedTflops = 130.0;   // chip-wide fp32 MFMA rate of the GEMM body, all slots busy
+constexpr double kSustainedTflops = 150.0;   // chip-wide fp32 rate of the GEMM body (split6), all slots busy
 constexpr double kSustainedTflopsBf16 = 300.0;   // the bf16-LDS body (conv_body_bf16), gather-bound
 
 ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {

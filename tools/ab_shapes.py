@@ -50,6 +50,49 @@ SHAPES = [  # (op, B, cin, H, cout, k, stride, pad, scaled, weight = launches pe
 ]
 
 
+def accuracy():
+    """AB_ACC=1: every shape's op at B = 2 against float64 on the host (torch autograd of the
+    replicate-padded conv): max |err| / max |ref| per shape."""
+    import torch
+    import torch.nn.functional as F
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from gan_amd import ops
+    dev = torch.device("cuda")
+    gen = torch.Generator().manual_seed(0)
+    worst = 0.0
+    for op, B, cin, H, cout, k, s, p, scaled, n in SHAPES:
+        B = 2
+        g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
+        x = torch.randn(B, cin, H, H, generator=gen, dtype=torch.float64, requires_grad=True)
+        w = torch.randn(cout, cin, k, k, generator=gen, dtype=torch.float64, requires_grad=True)
+        sx = torch.rand(cin, B, generator=gen, dtype=torch.float64) + 0.5 if scaled else None
+        sy = torch.rand(cout, B, generator=gen, dtype=torch.float64) + 0.5 if scaled else None
+        xm = x * sx.t()[:, :, None, None] if scaled else x
+        y = F.conv2d(F.pad(xm, (p, p, p, p), mode="replicate"), w, stride=s)
+        if scaled:
+            y = y * sy.t()[:, :, None, None]
+        gy = torch.randn(y.shape, generator=gen, dtype=torch.float64)
+        gx, gw = torch.autograd.grad(y, (x, w), gy)
+        cn = (lambda t: t.permute(1, 0, 2, 3).contiguous().float().to(dev))
+        f = (lambda t: None if t is None else t.float().to(dev))
+        with torch.no_grad():
+            if op == "fwd":
+                got, ref = ops._conv_fwd(g, cn(x.detach()), torch.nn.Parameter(f(w.detach())), None, f(sx), f(sy), 1.0), y
+                ref = ref.permute(1, 0, 2, 3)
+            elif op == "dgrad":
+                if scaled:
+                    continue
+                got, ref = ops._conv_dgrad(g, cn(gy), torch.nn.Parameter(f(w.detach())), None, 1.0), gx.permute(1, 0, 2, 3)
+            else:
+                if scaled:
+                    continue
+                got, ref = ops._conv_wgrad(g, cn(x.detach()), cn(gy), None, None, 1.0), gw
+        err = float((got.double().cpu() - ref.detach()).abs().max() / ref.detach().abs().max())
+        worst = max(worst, err)
+        print(f"  {op:5s} {cin:5d}->{cout:5d} {H:3d}^2 k{k} s{s} {'S' if scaled else ' '}  rel err {err:.2e}", flush=True)
+    print(f"  worst rel err {worst:.2e}", flush=True)
+
+
 def child():
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -88,7 +131,7 @@ def child():
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
-        child()
+        (accuracy if _os.environ.get("AB_ACC") else child)()
         sys.exit(0)
     rc = 0
     for arg in sys.argv[1:]:
