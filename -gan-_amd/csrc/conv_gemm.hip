@@ -282,7 +282,9 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 // are exact in fp32), so x is kept to 24 significant bits.  x * y is then the six bf16 products
 // with at least one high part -- hh + (hm + mh) + (hl + lh + mm) -- exact in the MFMA; the three
 // dropped ones (ml, lm, ll) are below 2^-24 |x y|, fp32's own rounding.  Six
-// v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) replace eight v_mfma_f32_32x32x2_f32 (8 x 64).
+// v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) replace eight v_mfma_f32_32x32x2_f32 (8 x 64); 16-row
+// blocks: six half-rate v_mfma_f32_16x16x16_bf16 here, three paired full-rate 16x16x32 in the LDS
+// body (mfma_tile_x3).
 #ifndef GANAMD_SPLIT6
 #define GANAMD_SPLIT6 1
 #endif
@@ -353,7 +355,11 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
       const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
       b[j][0] = t0[0]; b[j][1] = t0[1]; b[j][2] = t1[0]; b[j][3] = t1[1];
     }
-    if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT6_16) {   // 16x16x16 bf16: lane (r, q) holds A[r][4q..4q+3] -- this map
+
+    if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT6_16) {
+      // 16x16x16 bf16: lane (r, q) holds A[r][4q..4q+3] -- this map.  (Pairing the products on
+      // the full-rate 16x16x32 as mfma_tile_x3 does needs 8 k per lane: twice the fp32 LDS reads
+      // and splits here, measured 30 % slower on the 96-wide wgrad tiles.)
       bf16x4 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
 #pragma unroll
       for (int i = 0; i < C::TM; ++i) split3<4>(a[i], ah[i], am[i], al[i]);
@@ -776,7 +782,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const typename 
 }
 
 #ifndef GANAMD_CONV_WPE
-#define GANAMD_CONV_WPE 1
+#define GANAMD_CONV_WPE 3   // split6 LDS body: 3 waves/SIMD fit (<= 168 VGPRs, 3 x 49 KB LDS per CU)
 #endif
 #ifndef GANAMD_WGRAD_WPE
 #define GANAMD_WGRAD_WPE 1
@@ -795,29 +801,53 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p);
 #ifndef GANAMD_SPLIT_LDS
 #define GANAMD_SPLIT_LDS 1
 #endif
-constexpr int LDH = BK + 8;
+#ifndef GANAMD_X3_WIDE   // the 256-wide tiles of M <= 32 too (2 blocks per CU with 32-byte rows)
+#define GANAMD_X3_WIDE 1
+#endif
+#ifndef GANAMD_X3_SWZ
+#define GANAMD_X3_SWZ 1
+#endif
+// plane row stride (bf16 elements).  SWZ: 32-byte rows (no pad) with the two 16-byte halves of row
+// r swapped when bit 3 of r is set -- the same conflict-free fragment reads in two thirds of the LDS
+constexpr int LDH = GANAMD_X3_SWZ ? BK : BK + 8;
+// element offset of k-group `half` (8 k) of plane row r
+__device__ __forceinline__ int x3_off(int r, int half) {
+  return r * LDH + 8 * (GANAMD_X3_SWZ ? (half ^ ((r >> 3) & 1)) : half);
+}
 
 template <class C, int PSA, int PSB>
 __device__ __forceinline__ void mfma_tile_x3(const unsigned short* __restrict__ As, const unsigned short* __restrict__ Bs,
                                              typename C::acc_t (&acc)[C::TM][C::TN], int lane, int wm, int wn) {
-  if constexpr (C::MB == 16) {   // 16x16x16 bf16: lane (r, q) holds k = 4q .. 4q+3 of row r
-    const int r = lane & 15, q = lane >> 4;
-    bf16x4 a[C::TM][3], b[C::TN][3];
+  if constexpr (C::MB == 16) {
+    // full-rate v_mfma_f32_16x16x32_bf16 on PAIRS of split products: its 32 k are two 16-k halves
+    // (lane (r, q) holds k = 8q .. 8q+7: q < 2 the first half, q >= 2 the second), so
+    // (h|m)x(h|h) = hh + mh, (h|l)x(m|h) = hm + lh, (m|h)x(m|l) = mm + hl -- three instructions
+    // for the six products where 16x16x16 would need six at half the rate
+    const int r = lane & 15, q = lane >> 4, hf = q & 1, hi = q >> 1;
+    const int a0 = hi ? PSA : 0, a1 = hi ? 2 * PSA : 0, a2 = hi ? 0 : PSA;   // plane offsets of this
+    const int b0 = 0, b1 = hi ? 0 : PSB, b2 = hi ? 2 * PSB : PSB;           // lane's k-half
+    bf16x8 a[C::TM][3], b[C::TN][3];
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i)
+    for (int i = 0; i < C::TM; ++i) {
+      const int o = x3_off((wm * C::TM + i) * 16 + r, hf);
+      a[i][0] = *reinterpret_cast<const bf16x8*>(&As[a0 + o]);   // (h | m)
+      a[i][1] = *reinterpret_cast<const bf16x8*>(&As[a1 + o]);   // (h | l)
+      a[i][2] = *reinterpret_cast<const bf16x8*>(&As[a2 + o]);   // (m | h)
+    }
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        a[i][pl] = *reinterpret_cast<const bf16x4*>(&As[pl * PSA + ((wm * C::TM + i) * 16 + r) * LDH + 4 * q]);
-#pragma unroll
-    for (int j = 0; j < C::TN; ++j)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        b[j][pl] = *reinterpret_cast<const bf16x4*>(&Bs[pl * PSB + ((wn * C::TN + j) * 16 + r) * LDH + 4 * q]);
+    for (int j = 0; j < C::TN; ++j) {
+      const int o = x3_off((wn * C::TN + j) * 16 + r, hf);
+      b[j][0] = *reinterpret_cast<const bf16x8*>(&Bs[b0 + o]);   // (h | h)
+      b[j][1] = *reinterpret_cast<const bf16x8*>(&Bs[b1 + o]);   // (m | h)
+      b[j][2] = *reinterpret_cast<const bf16x8*>(&Bs[b2 + o]);   // (m | l)
+    }
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
       for (int j = 0; j < C::TN; ++j)
-        acc[i][j] = mfma6_16(a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2], acc[i][j]);
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
   } else {                       // 32x32x16 bf16: lane (r, h) holds k = 8h .. 8h+7 of row r
     const int r = lane & 31, h = lane >> 5;
     bf16x8 a[C::TM][3], b[C::TN][3];
@@ -825,12 +855,12 @@ __device__ __forceinline__ void mfma_tile_x3(const unsigned short* __restrict__ 
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        a[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl * PSA + ((wm * C::TM + i) * 32 + r) * LDH + 8 * h]);
+        a[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl * PSA + x3_off((wm * C::TM + i) * 32 + r, h)]);
 #pragma unroll
     for (int j = 0; j < C::TN; ++j)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        b[j][pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl * PSB + ((wn * C::TN + j) * 32 + r) * LDH + 8 * h]);
+        b[j][pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl * PSB + x3_off((wn * C::TN + j) * 32 + r, h)]);
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
@@ -959,7 +989,7 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
       if (slot < SA) {
         const float v[8] = {S.ra[e][0][0], S.ra[e][0][1], S.ra[e][0][2], S.ra[e][0][3],
                             S.ra[e][1][0], S.ra[e][1][1], S.ra[e][1][2], S.ra[e][1][3]};
-        store_split8<PSA>(&As[buf][(slot / SPR) * LDH + 8 * (slot % SPR)], v);
+        store_split8<PSA>(&As[buf][x3_off(slot / SPR, slot % SPR)], v);
       }
     }
 #pragma unroll
@@ -967,7 +997,7 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
       float v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = BSCALE ? S.rb[e + q] * S.rs[e + q] : S.rb[e + q];
-      store_split8<PSB>(&Bs[buf][b_n * LDH + b_kg * KPT + e], v);
+      store_split8<PSB>(&Bs[buf][x3_off(b_n, (b_kg * KPT + e) / 8)], v);
     }
   };
 
@@ -999,7 +1029,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD
 void conv_gemm_kernel(ConvArgs p) {
   if constexpr (BF16) {
     conv_body_bf16<BM, BN, WGM, WGN, MODE, BSCALE>(p);
-  } else if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT_LDS) {
+  } else if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT_LDS && (BN == 128 || GANAMD_X3_WIDE)) {
     conv_body_x3<BM, BN, WGM, WGN, MODE, BSCALE>(p);
   } else {
     conv_body_f32<BM, BN, WGM, WGN, MODE, BSCALE>(p);
