@@ -46,6 +46,22 @@ class PackJob(ctypes.Structure):
                [("chunk0", ctypes.c_int64)]
 
 
+class CriticOp(ctypes.Structure):
+    """ganamd_critic_op (include/ganamd.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("ins", ctypes.c_int32 * 3)] + \
+               [(n, ctypes.c_int32) for n in ("cout", "k", "stride", "pad", "pad_mode", "n_out", "kr", "akr",
+                                              "group")] + \
+               [("alpha", ctypes.c_float)] + \
+               [(n, ctypes.c_void_p) for n in ("w", "w_fwd", "w_dgrad", "bias", "ri", "rw", "ari", "arw")]
+
+
+class CriticGrads(ctypes.Structure):
+    _fields_ = [("gw", ctypes.c_void_p), ("gb", ctypes.c_void_p)]
+
+
+COP = {k: i for i, k in enumerate(("swap", "conv", "prelu", "resample", "pmean", "sigmoid", "scale_add", "mbstd",
+                                   "flatten"))}
+
 # name -> (restype, argtypes)
 _SIGS = {
     "ganamd_version": (ctypes.c_char_p, []),
@@ -108,6 +124,15 @@ _SIGS = {
     "ganamd_philox_normal": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_draw": (c_int, [vp, c_long, ctypes.c_uint64, vp, ctypes.c_uint32, c_int, c_int, vp]),
     "ganamd_philox_advance": (c_int, [vp, vp]),
+    "ganamd_critic_create": (vp, [ctypes.POINTER(CriticOp), c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "ganamd_critic_destroy": (None, [vp]),
+    "ganamd_critic_workspace": (c_int, [vp, ctypes.POINTER(c_size_t)]),
+    "ganamd_critic_value": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ganamd_critic_forward": (c_int, [vp, vp, vp, vp, vp]),
+    "ganamd_critic_backward": (c_int, [vp, vp, vp, vp, vp, vp]),
+    "ganamd_critic_tangent": (c_int, [vp, vp, vp, vp, vp]),
+    "ganamd_critic_adjoint": (c_int, [vp, vp, vp, vp, vp, vp]),
+    "ganamd_critic_gp_step": (c_int, [vp, vp, c_float, c_float, c_int, vp, vp, vp, vp, vp, vp, vp]),
     "ganamd_image_batch_workspace": (c_size_t, [c_int, c_int, c_int]),
     "ganamd_image_batch": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, c_int, c_int, vp, vp, c_int, c_int, vp, vp,
                                    vp, vp, vp]),

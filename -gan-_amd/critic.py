@@ -25,6 +25,12 @@ backward, one tangent forward, one adjoint backward and two weight-gradient GEMM
 nothing is taped at run time beyond the saved activations, no per-layer autograd nodes run, and
 dead work (weight gradients inside ``autograd.grad``) is never issued.
 
+The sweeps run inside libganamd.so (csrc/critic.hip, the ganamd_critic_* C ABI; one
+ganamd_critic_gp_step call is the whole GP double backward for a non-Python host, INTEGRATION.md
+§4).  This module builds the program of a Discriminator, hands the engine its op table (weights,
+GEMM-order packed copies from ops.PackCache, resampling tables) and one workspace per evaluation,
+and puts the reference's autograd protocol on top.
+
 Entry points:
   * ``critic_forward(D, x, segments)`` -- the drop-in ``Discriminator.forward``: one autograd
     node (``_CriticFn``) whose backward is the explicit backward sweep and is itself
@@ -137,47 +143,8 @@ def program_of(D) -> Program:
 
 
 # ------------------------------------------------------------------------------------------
-# kernels of one op (thin wrappers; all launch on torch's current stream)
+# the op table of the C-ABI engine (include/ganamd.h "Critic program engine", csrc/critic.hip)
 # ------------------------------------------------------------------------------------------
-
-
-def _conv_parts(mod):
-    """(weight, bias, alpha, k, stride, pad) of an EqualizedConv2d / EqualizedLinear."""
-    w = mod.weight.weight
-    return w, mod.bias, mod.weight.c
-
-
-def _geo(op, x):
-    m = op.mod
-    if op.kind == "linear":
-        cin, B = x.shape
-        return ops.linear_geo(B, cin, m.weight.weight.shape[0])
-    C, B, H, W = x.shape
-    return ops.conv_geo(B, C, H, W, m.bias.shape[0], m.k, m.stride, m.padding)
-
-
-def _w4(op):
-    w = op.mod.weight.weight
-    return w if w.dim() == 4 else w.view(w.shape[0], w.shape[1], 1, 1)
-
-
-def _as4(op, t, geo, out=False):
-    if op.kind != "linear":
-        return t
-    c = geo.Cout if out else geo.Cin
-    return t.view(c, geo.B, 1, 1)
-
-
-def _as2(op, t):
-    return t.view(t.shape[0], t.shape[1]) if op.kind == "linear" else t
-
-
-def _rows(t):
-    return t.shape[0], t.numel() // t.shape[0]
-
-
-def _planes(t):
-    return t.shape[0] * t.shape[1], t.numel() // (t.shape[0] * t.shape[1])
 
 
 def _grad_buf(p):
@@ -190,108 +157,75 @@ def _grad_buf(p):
     return g
 
 
-def _prelu_fwd(x, a):
-    C, L = _rows(x)
-    y = torch.empty_like(x)
-    check(LIB.ganamd_prelu_fwd(ptr(x), ptr(a), C, L, ptr(y), stream()), "prelu_fwd")
-    return y
+def _w4(op):
+    w = op.mod.weight.weight
+    return w if w.dim() == 4 else w.view(w.shape[0], w.shape[1], 1, 1)
 
 
-def _prelu_bwd(gy, x, a, galpha):
-    C, L = _rows(x)
-    gx = torch.empty_like(x)
-    ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device) if galpha is not None else None
-    check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), ptr(galpha), 1, ptr(ws), stream()),
-          "prelu_bwd")
-    return gx
+def _shapes(prog, C0, H0, W0):
+    """(C, H, W) per value (value 0: the NCHW input), as ganamd_critic_create derives them."""
+    sh = {0: (C0, H0, W0)}
+    for op in prog.ops:
+        C, H, W = sh[op.ins[0]]
+        k = op.kind
+        if k == "conv":
+            m = op.mod
+            sh[op.out] = (m.bias.shape[0], (H + 2 * m.padding - m.k) // m.stride + 1,
+                          (W + 2 * m.padding - m.k) // m.stride + 1)
+        elif k == "linear":
+            sh[op.out] = (op.mod.weight.weight.shape[0], 1, 1)
+        elif k == "resample":
+            sh[op.out] = (C, tables.table(op.arg, H, "cpu").n_out, tables.table(op.arg, H, "cpu").n_out)
+        elif k == "pmean":
+            sh[op.out] = (C, 1, 1)
+        elif k == "mbstd":
+            sh[op.out] = (C + 1, H, W)
+        elif k == "flatten":
+            sh[op.out] = (C * H * W, 1, 1)
+        else:
+            sh[op.out] = (C, H, W)
+    return sh
 
 
-def _prelu_tangent(xd, gy, x, a, galpha):
-    C, L = _rows(x)
-    yd = torch.empty_like(x)
-    ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device) if galpha is not None else None
-    check(LIB.ganamd_prelu_tangent(ptr(xd), ptr(gy), ptr(x), ptr(a), C, L, ptr(yd), ptr(galpha), 1, ptr(ws),
-                                   stream()), "prelu_tangent")
-    return yd
+def _geo_of(op, B, shape_in):
+    C, H, W = shape_in
+    m = op.mod
+    if op.kind == "linear":
+        return ops.linear_geo(B, C, m.weight.weight.shape[0])
+    return ops.conv_geo(B, C, H, W, m.bias.shape[0], m.k, m.stride, m.padding)
 
 
-def _resample(x, kind):
-    tab = tables.table(kind, x.shape[2], x.device)
-    return ops._resample(x, tab.n_in, tab.n_out, tab.fwd)
-
-
-def _resample_adj(gy, kind, n_in):
-    """adjoint (backward) of resampler ``kind`` whose forward input was n_in x n_in"""
-    tab = tables.table(kind, n_in, gy.device)
-    return ops._resample(gy, tab.n_out, tab.n_in, tab.adj)
-
-
-def _pmean(x):
-    C, B, H, W = x.shape
-    if H * W == 1:
-        return x.reshape(C, B)
-    out = torch.empty((C, B), device=x.device, dtype=torch.float32)
-    check(LIB.ganamd_plane_dot(ptr(x), None, C * B, H * W, 1.0 / (H * W), ptr(out), stream()), "plane_dot")
-    return out
-
-
-def _pmean_adj(g, shape):
-    C, B, H, W = shape
-    if H * W == 1:
-        return g.reshape(C, B, 1, 1)
-    return (g * (1.0 / (H * W))).reshape(C, B, 1, 1).expand(C, B, H, W).contiguous()
-
-
-def _act(kind, x):
-    y = torch.empty_like(x)
-    check(LIB.ganamd_act_fwd(kind, ptr(x), x.numel(), 0.0, ptr(y), stream()), "act_fwd")
-    return y
-
-
-def _act_bwd(kind, v, gy):
-    gx = torch.empty_like(v)
-    check(LIB.ganamd_act_bwd(kind, ptr(v), ptr(gy), v.numel(), 0.0, ptr(gx), stream()), "act_bwd")
-    return gx
-
-
-def _act_adjoint(kind, v, ay, gy, xd):
-    ax = torch.empty_like(v)
-    check(LIB.ganamd_act_adjoint(kind, ptr(v), ptr(ay), ptr(gy), ptr(xd), v.numel(), 0.0, ptr(ax), stream()),
-          "act_adjoint")
-    return ax
-
-
-def _scale_add2(x1, s1, x2=None, s2=None, r=None):
-    P, HW = _planes(x1)
-    y = torch.empty_like(x1)
-    check(LIB.ganamd_scale_add2(ptr(x1), ptr(s1), ptr(x2), ptr(s2), ptr(r), P, HW, ptr(y), stream()), "scale_add2")
-    return y
-
-
-def _plane_dot2(a1, b1, a2=None, b2=None):
-    P, HW = _planes(a1)
-    out = torch.empty(a1.shape[:2], device=a1.device, dtype=torch.float32)
-    check(LIB.ganamd_plane_dot2(ptr(a1), ptr(b1), ptr(a2), ptr(b2), P, HW, ptr(out), stream()), "plane_dot2")
-    return out
-
-
-def _axpy(x, y, a=1.0):
-    check(LIB.ganamd_axpy(y.numel(), float(a), ptr(x), ptr(y), stream()), "axpy")
-
-
-def _swap(x):
-    return x.permute(1, 0, 2, 3).contiguous()
-
-
-def _flatten(x):
-    """[C,B,H,W] -> [(c,h,w), B]: the NCHW .view(B, -1) feature order of discriminator_9_4.py:197."""
-    C, B, H, W = x.shape
-    return x.permute(0, 2, 3, 1).reshape(C * H * W, B).contiguous()
-
-
-def _unflatten(z, shape):
-    C, B, H, W = shape
-    return z.view(C, H, W, B).permute(0, 3, 1, 2).contiguous()
+def _op_table(prog, B, sh, device, keep):
+    """ctypes ganamd_critic_op[] of the program at batch B (packed weight copies from the cache)."""
+    t = (_lib.CriticOp * len(prog.ops))()
+    for i, op in enumerate(prog.ops):
+        e = t[i]
+        e.kind = _lib.COP["conv" if op.kind == "linear" else op.kind]
+        ins = list(op.ins) + [-1] * (3 - len(op.ins))
+        for j in range(3):
+            e.ins[j] = ins[j]
+        if op.kind in ("conv", "linear"):
+            m = op.mod
+            geo = _geo_of(op, B, sh[op.ins[0]])
+            w = _w4(op)
+            pf = ops.PackCache.get(geo, _lib.CONV_FWD, w)
+            pd = ops.PackCache.get(geo, _lib.CONV_DGRAD, w)
+            keep += [w, pf, pd, m.bias]
+            e.cout, e.k, e.stride, e.pad, e.pad_mode = geo.Cout, geo.K, geo.stride, geo.pad, geo.pad_mode
+            e.alpha = float(m.weight.c)
+            e.w, e.w_fwd, e.w_dgrad, e.bias = ptr(w), ptr(pf), ptr(pd), ptr(m.bias)
+        elif op.kind == "prelu":
+            e.w = ptr(op.mod.weight)
+            keep.append(op.mod.weight)
+        elif op.kind == "resample":
+            tab = tables.table(op.arg, sh[op.ins[0]][1], device)
+            (fi, fw, fk), (ai, aw, ak) = tab.fwd, tab.adj
+            keep.append(tab)
+            e.n_out, e.kr, e.akr = tab.n_out, fk, ak
+            e.ri, e.rw, e.ari, e.arw = _lib.iptr(fi), ptr(fw), _lib.iptr(ai), ptr(aw)
+        elif op.kind == "mbstd":
+            e.group = op.mod.group_size
+    return t
 
 
 # ------------------------------------------------------------------------------------------
@@ -299,246 +233,149 @@ def _unflatten(z, shape):
 # ------------------------------------------------------------------------------------------
 
 
+class _Values:
+    """Read access to one sweep's values (0 X, 1 G, 2 XD, 3 A) as views of the run's workspace."""
+
+    def __init__(self, run, which):
+        self.run, self.which = run, which
+
+    def __getitem__(self, v):
+        run = self.run
+        p = _lib.ctypes.c_void_p()
+        check(LIB.ganamd_critic_value(run.plan, self.which, int(v), _lib.ctypes.byref(p)), "critic_value")
+        if not p.value:
+            raise KeyError(v)
+        if v == 0:
+            return run.x if self.which == 0 else run.v
+        C, H, W = run.sh[v]
+        off = (p.value - run.ws.data_ptr()) // 4
+        n = C * run.B * H * W
+        if off < 0 or off + n > run.ws.numel():
+            raise _lib.GanAmdError(f"critic value {v} outside the run's workspace")
+        t = run.ws[off:off + n]
+        # per-sample vectors (linear / pool / flatten outputs and activations of them) are [C, B];
+        # maps (a 1x1 conv output included) [C, B, H, W]
+        return t.view(C, run.B) if run.vec[v] else t.view(C, run.B, H, W)
+
+    def get(self, v, default=None):
+        try:
+            return self[v]
+        except KeyError:
+            return default
+
+
 class Run:
-    """Saved activations (X), first-order gradients (G), tangents (XD) and adjoints (A) of one
-    critic evaluation, and the sweeps over them."""
+    """One critic evaluation through the C-ABI engine (ganamd_critic_*): the plan of the program
+    at this batch, the workspace holding every saved activation, gradient, tangent and adjoint,
+    and the sweeps.  ``X`` / ``G`` / ``XD`` read values back (tests, tools)."""
 
     def __init__(self, prog: Program, segments: int = 1):
         self.prog = prog
         self.segments = segments
-        self.X: dict = {}
-        self.G: dict = {}
-        self.XD: dict = {}
-        self.borrowed: set = set()
+        self.plan = None
+        self.ws = None
+        self.keep = []
+        self.x = self.v = None
+        self.X, self.G, self.XD = _Values(self, 0), _Values(self, 1), _Values(self, 2)
 
-    # ---------------------------------------------------------------- forward
-    def forward(self, x_nchw):
-        X = self.X
-        X[0] = x_nchw
+    def __del__(self):
+        if self.plan:
+            LIB.ganamd_critic_destroy(self.plan)
+            self.plan = None
+
+    def _setup(self, x):
+        B, C, H, W = x.shape
+        self.B = B
+        self.sh = _shapes(self.prog, C, H, W)
+        self.vec = {0: False}
         for op in self.prog.ops:
-            X[op.out] = self._fwd(op, [X[i] for i in op.ins])
-        return X[self.prog.out]
+            self.vec[op.out] = op.kind in ("linear", "pmean", "flatten") or (
+                op.kind in ("prelu", "sigmoid") and self.vec[op.ins[0]])
+        self.table = _op_table(self.prog, B, self.sh, x.device, self.keep)
+        self.plan = LIB.ganamd_critic_create(self.table, len(self.prog.ops), B, C, H, W, self.segments, ops._MATH[0])
+        if not self.plan:
+            raise _lib.GanAmdError(f"critic program rejected by ganamd_critic_create (B={B}, segments={self.segments})")
+        n = _lib.c_size_t(0)
+        check(LIB.ganamd_critic_workspace(self.plan, _lib.ctypes.byref(n)), "critic_workspace")
+        self.ws = workspace(n.value, x.device)
 
-    def _fwd(self, op, xs):
-        k = op.kind
-        x = xs[0]
-        if k == "swap":
-            return _swap(x)
-        if k in ("conv", "linear"):
-            geo = _geo(op, x)
-            w, b, c = _conv_parts(op.mod)
-            y = ops._conv_fwd(geo, _as4(op, x, geo), _w4(op), b, alpha=c)
-            return _as2(op, y)
-        if k == "prelu":
-            return _prelu_fwd(x, op.mod.weight)
-        if k == "resample":
-            return _resample(x, op.arg)
-        if k == "pmean":
-            return _pmean(x)
-        if k == "sigmoid":
-            return _act(_lib.ACT_SIGMOID, x)
-        if k == "scale_add":
-            return _scale_add2(xs[0], xs[1], r=xs[2])
-        if k == "mbstd":
-            C, B, H, W = x.shape
-            y = torch.empty((C + 1, B, H, W), device=x.device, dtype=torch.float32)
-            ws = workspace(LIB.ganamd_mbstd_workspace(self.segments), x.device)
-            check(LIB.ganamd_mbstd_fwd(ptr(x), B * H * W, C, B, H * W, self.segments, 4, ptr(y), B * H * W, None,
-                                       ptr(ws), stream()), "mbstd_fwd")
-            return y
-        if k == "flatten":
-            return _flatten(x)
-        raise _lib.GanAmdError(f"unknown critic op {k}")
+    def _grads(self):
+        """ganamd_critic_grads[] of the parameters that want a gradient (created as zeros)."""
+        g = (_lib.CriticGrads * len(self.prog.ops))()
+        for i, op in enumerate(self.prog.ops):
+            if op.kind in ("conv", "linear"):
+                w, b = op.mod.weight.weight, op.mod.bias
+                if w.requires_grad:
+                    g[i].gw = ptr(_grad_buf(w))
+                if b is not None and b.requires_grad:
+                    g[i].gb = ptr(_grad_buf(b))
+            elif op.kind == "prelu" and op.mod.weight.requires_grad:
+                g[i].gw = ptr(_grad_buf(op.mod.weight))
+        return g
 
-    # ---------------------------------------------------------------- accumulation
-    def _acc(self, D, v, t, borrowed=False):
-        """D[v] += t.  A tensor that is also another value's gradient (an identity pass-through)
-        is held 'borrowed' and never written in place."""
-        if v not in D:
-            D[v] = t
-            if borrowed:
-                self.borrowed.add((id(D), v))
+    def _count(self, sweep, params=False, need_input=False, seeded=False):
+        """The sweep's conv GEMMs into ops.FlopCounter (host-side bookkeeping of the bench)."""
+        if not ops.FlopCounter.enabled and ops.FlopCounter.record is None:
             return
-        key = (id(D), v)
-        if key in self.borrowed:
-            if borrowed:        # both borrowed: materialise a sum
-                s = t.clone()
-                _axpy(D[v], s)
-                D[v] = s
-            else:
-                _axpy(D[v], t)  # t is fresh: add the borrowed one into it
-                D[v] = t
-            self.borrowed.discard(key)
+        convs = [op for op in self.prog.ops if op.kind in ("conv", "linear")]
+        if sweep in ("forward", "tangent"):
+            for op in convs:
+                ops.FlopCounter.add(_geo_of(op, self.B, self.sh[op.ins[0]]), "fwd")
             return
-        _axpy(t, D[v])
-
-    # ---------------------------------------------------------------- first-order backward
-    def backward(self, seed, params: bool, need_input: bool):
-        """g_v for every value from g_out = seed; parameter gradients accumulated into .grad when
-        ``params``; the input gradient (NCHW) returned when ``need_input``."""
-        G = self.G
-        G.clear()
-        self.borrowed.clear()
-        G[self.prog.out] = seed
-        X = self.X
+        # which values carry an adjoint (the backward: all; the adjoint: from the seed and the
+        # second-order sources -- sigmoid, the SE product, MiniBatchStdDev -- downwards)
+        has = {self.prog.out} if (sweep == "backward" or seeded) else set()
         for op in reversed(self.prog.ops):
-            gy = G.get(op.out)
-            if gy is None:
-                continue
-            k = op.kind
-            x = X[op.ins[0]]
-            first = op.ins[0] == 1 and k in ("conv",)   # the stem conv reads the swapped input
-            if k == "swap":
-                if need_input:
-                    G[0] = _swap(gy)
-            elif k in ("conv", "linear"):
-                geo = _geo(op, x)
-                w, b, c = _conv_parts(op.mod)
-                if not first or need_input:
-                    gx = ops._conv_dgrad(geo, _as4(op, gy, geo, out=True), _w4(op), alpha=c)
-                    self._acc(G, op.ins[0], _as2(op, gx))
-                if params and w.requires_grad:
-                    ops._conv_wgrad(geo, _as4(op, x, geo), _as4(op, gy, geo, out=True), alpha=c,
-                                    out=_grad_buf(w), accumulate=True)
-                    ops.row_sum_acc(gy, _grad_buf(b))
-            elif k == "prelu":
-                a = op.mod.weight
-                self._acc(G, op.ins[0], _prelu_bwd(gy, x, a, _grad_buf(a) if params and a.requires_grad else None))
-            elif k == "resample":
-                self._acc(G, op.ins[0], _resample_adj(gy, op.arg, x.shape[2]))
-            elif k == "pmean":
-                self._acc(G, op.ins[0], _pmean_adj(gy, x.shape), borrowed=x.shape[2] * x.shape[3] == 1)
-            elif k == "sigmoid":
-                self._acc(G, op.ins[0], _act_bwd(_lib.ACT_SIGMOID, X[op.out], gy))
-            elif k == "scale_add":
-                xv, s, r = op.ins
-                self._acc(G, xv, _scale_add2(gy, X[s]))
-                self._acc(G, s, _plane_dot2(gy, X[xv]))
-                self._acc(G, r, gy, borrowed=True)
-            elif k == "mbstd":
-                C, B, H, W = x.shape
-                gx = torch.empty_like(x)
-                ws = workspace(LIB.ganamd_mbstd_workspace(self.segments), x.device)
-                check(LIB.ganamd_mbstd_bwd(ptr(x), B * H * W, ptr(gy), B * H * W, C, B, H * W, self.segments, 4,
-                                           ptr(gx), ptr(ws), stream()), "mbstd_bwd")
-                self._acc(G, op.ins[0], gx)
-            elif k == "flatten":
-                self._acc(G, op.ins[0], _unflatten(gy, x.shape))
-        return G.get(0)
+            live = op.out in has or (sweep == "adjoint" and op.kind in ("sigmoid", "mbstd"))
+            if op.kind in ("conv", "linear"):
+                geo = _geo_of(op, self.B, self.sh[op.ins[0]])
+                first = self.prog.ops[op.ins[0] - 1].kind == "swap" if op.ins[0] > 0 else True
+                if op.out in has and (not first or need_input):
+                    ops.FlopCounter.add(geo, "dgrad")
+                if params and op.mod.weight.weight.requires_grad:
+                    for _ in range((op.out in has) + (sweep == "adjoint")):
+                        ops.FlopCounter.add(geo, "wgrad")
+            if live:
+                has.update(op.ins)
+            elif sweep == "adjoint" and op.kind == "scale_add":     # G-terms only: x and the gate
+                has.update(op.ins[:2])
 
-    # ---------------------------------------------------------------- tangent (forward-mode)
+    # ---------------------------------------------------------------- sweeps
+    def forward(self, x_nchw):
+        self.x = x_nchw
+        self._setup(x_nchw)
+        self._count("forward")
+        check(LIB.ganamd_critic_forward(self.plan, ptr(x_nchw), None, ptr(self.ws), stream()), "critic_forward")
+        return self.X[self.prog.out].clone()               # [1, B], not a view of the workspace
+
+    def backward(self, seed, params: bool, need_input: bool):
+        """g_v for every value from g_out = seed ([1, B]); parameter gradients accumulated into
+        .grad when ``params``; the input gradient (NCHW) returned when ``need_input``."""
+        self._count("backward", params, need_input)
+        self.seed = seed.contiguous()
+        gx = torch.empty_like(self.x) if need_input else None
+        check(LIB.ganamd_critic_backward(self.plan, ptr(self.seed), self._grads() if params else None, ptr(gx),
+                                         ptr(self.ws), stream()), "critic_backward")
+        return gx
+
     def tangent(self, v_nchw, params: bool):
-        """xd_v along the input direction v; the PReLU slopes' second-order term (needs G)
-        accumulates into their gradients when ``params``."""
-        XD, X, G = self.XD, self.X, self.G
-        XD.clear()
-        XD[0] = v_nchw
-        for op in self.prog.ops:
-            k = op.kind
-            xd = XD[op.ins[0]]
-            x = X[op.ins[0]]
-            if k == "swap":
-                XD[op.out] = _swap(xd)
-            elif k in ("conv", "linear"):
-                geo = _geo(op, x)
-                w, b, c = _conv_parts(op.mod)
-                XD[op.out] = _as2(op, ops._conv_fwd(geo, _as4(op, xd, geo), _w4(op), None, alpha=c))
-            elif k == "prelu":
-                a = op.mod.weight
-                XD[op.out] = _prelu_tangent(xd, G[op.out], x, a, _grad_buf(a) if params and a.requires_grad else None)
-            elif k == "resample":
-                XD[op.out] = _resample(xd, op.arg)
-            elif k == "pmean":
-                XD[op.out] = _pmean(xd)
-            elif k == "sigmoid":
-                XD[op.out] = _act_bwd(_lib.ACT_SIGMOID, X[op.out], xd)
-            elif k == "scale_add":
-                xv, s, r = op.ins
-                XD[op.out] = _scale_add2(XD[xv], X[s], X[xv], XD[s], XD[r])
-            elif k == "mbstd":
-                C, B, H, W = x.shape
-                yd = torch.empty((C + 1, B, H, W), device=x.device, dtype=torch.float32)
-                ws = workspace(LIB.ganamd_mbstd_workspace(self.segments), x.device)
-                check(LIB.ganamd_mbstd_tangent(ptr(x), ptr(xd), B * H * W, C, B, H * W, self.segments, 4, ptr(yd),
-                                               B * H * W, ptr(ws), stream()), "mbstd_tangent")
-                XD[op.out] = yd
-            elif k == "flatten":
-                XD[op.out] = _flatten(xd)
-        return XD[self.prog.out]
+        """xd_v along the input direction v; the PReLU slopes' second-order term accumulates into
+        their gradients when ``params``."""
+        self._count("tangent")
+        self.v = v_nchw.contiguous()
+        check(LIB.ganamd_critic_tangent(self.plan, ptr(self.v), self._grads() if params else None, ptr(self.ws),
+                                        stream()), "critic_tangent")
+        return self.XD[self.prog.out]
 
-    # ---------------------------------------------------------------- adjoint (second-order reverse)
     def adjoint(self, a_seed, params: bool, need_input: bool = False):
         """Reverse sweep of h = <v, g> (+ <a_seed, D(x)>): accumulates dh/dtheta into the
-        parameters' gradients; returns dh/dx (NCHW) when ``need_input``.  a_seed may be None
-        (pure penalty)."""
-        A: dict = {}
-        X, G, XD = self.X, self.G, self.XD
-        self.borrowed.clear()
-        if a_seed is not None:
-            A[self.prog.out] = a_seed
-        for op in reversed(self.prog.ops):
-            k = op.kind
-            ay = A.pop(op.out, None)
-            gy = G.get(op.out)
-            x = X[op.ins[0]]
-            if k == "swap":
-                if need_input and ay is not None:
-                    A[0] = _swap(ay)
-            elif k in ("conv", "linear"):
-                geo = _geo(op, x)
-                w, b, c = _conv_parts(op.mod)
-                first = op.ins[0] == 1
-                if ay is not None and (not first or need_input):
-                    gx = ops._conv_dgrad(geo, _as4(op, ay, geo, out=True), _w4(op), alpha=c)
-                    self._acc(A, op.ins[0], _as2(op, gx))
-                if params and w.requires_grad:
-                    gw = _grad_buf(w)
-                    if ay is not None:
-                        ops._conv_wgrad(geo, _as4(op, x, geo), _as4(op, ay, geo, out=True), alpha=c, out=gw,
-                                        accumulate=True)
-                        ops.row_sum_acc(ay, _grad_buf(b))
-                    if gy is not None:
-                        ops._conv_wgrad(geo, _as4(op, XD[op.ins[0]], geo), _as4(op, gy, geo, out=True), alpha=c,
-                                        out=gw, accumulate=True)
-            elif k == "prelu":
-                if ay is not None:
-                    a = op.mod.weight
-                    self._acc(A, op.ins[0],
-                              _prelu_bwd(ay, x, a, _grad_buf(a) if params and a.requires_grad else None))
-            elif k == "resample":
-                if ay is not None:
-                    self._acc(A, op.ins[0], _resample_adj(ay, op.arg, x.shape[2]))
-            elif k == "pmean":
-                if ay is not None:
-                    self._acc(A, op.ins[0], _pmean_adj(ay, x.shape), borrowed=x.shape[2] * x.shape[3] == 1)
-            elif k == "sigmoid":
-                if ay is None:
-                    ay = torch.zeros_like(x)
-                self._acc(A, op.ins[0], _act_adjoint(_lib.ACT_SIGMOID, X[op.out], ay, gy, XD[op.ins[0]]))
-            elif k == "scale_add":
-                xv, s, r = op.ins
-                if ay is None:
-                    self._acc(A, xv, _scale_add2(gy, XD[s]))
-                    self._acc(A, s, _plane_dot2(gy, XD[xv]))
-                else:
-                    self._acc(A, xv, _scale_add2(ay, X[s], gy, XD[s]))
-                    self._acc(A, s, _plane_dot2(ay, X[xv], gy, XD[xv]))
-                    self._acc(A, r, ay, borrowed=True)
-            elif k == "mbstd":
-                C, B, H, W = x.shape
-                if ay is None:
-                    ay = torch.zeros_like(gy)
-                ax = torch.empty_like(x)
-                ws = workspace(LIB.ganamd_mbstd_workspace(self.segments), x.device)
-                check(LIB.ganamd_mbstd_adjoint(ptr(x), ptr(XD[op.ins[0]]), B * H * W, ptr(gy), ptr(ay), B * H * W, C,
-                                               B, H * W, self.segments, 4, ptr(ax), ptr(ws), stream()),
-                      "mbstd_adjoint")
-                self._acc(A, op.ins[0], ax)
-            elif k == "flatten":
-                if ay is not None:
-                    self._acc(A, op.ins[0], _unflatten(ay, x.shape))
-        return A.get(0)
-
+        parameters' gradients; returns dh/dx (NCHW) when ``need_input``.  a_seed may be None."""
+        self._count("adjoint", params, need_input, seeded=a_seed is not None)
+        self.a_seed = None if a_seed is None else a_seed.contiguous()
+        ax = torch.empty_like(self.x) if need_input else None
+        check(LIB.ganamd_critic_adjoint(self.plan, ptr(self.a_seed), self._grads() if params else None, ptr(ax),
+                                        ptr(self.ws), stream()), "critic_adjoint")
+        return ax
 
 # ------------------------------------------------------------------------------------------
 # the penalty on the input gradient
@@ -606,9 +443,7 @@ class _CriticGrad(Function):
     @staticmethod
     def forward(ctx, seed, run, first_order_params, *params):
         ctx.run, ctx.params = run, params
-        gx = run.backward(seed, params=first_order_params, need_input=True)
-        run.G.pop(0, None)     # the run must not hold this node's output (ctx -> run -> output cycle)
-        return gx
+        return run.backward(seed, params=first_order_params, need_input=True)   # not kept by the run
 
     @staticmethod
     @torch.autograd.function.once_differentiable

@@ -393,6 +393,108 @@ int ganamd_philox_draw(float* out, long n, uint64_t seed, uint64_t* offset, uint
                        hipStream_t stream);
 int ganamd_philox_advance(uint64_t* offset, hipStream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Critic program engine: the critic as a straight-line layer program, and the gradient
+ * penalty's double backward as C-ABI sweeps over it (csrc/critic.hip).
+ * Replaces the critic step's autograd protocol: train/wgangp.py:45-54 (compute_grad2:
+ *   autograd.grad(d_out.sum(), x_hat, create_graph=True) then grad.pow(2)...),
+ *   wgangp.py:34-43 (gradient_penalty), wgangp.py:68-69 (gp.backward() = the double backward),
+ *   train/wganlazygpR2.py:48-77 (R1 / R2 / GP on stacked segments).
+ * Program ops (value ids: value 0 is the NCHW input [B][C0][H0][W0]; every other value is CNHW
+ * [C][B][H][W], H = W = 1 for per-sample vectors):
+ *   SWAP       NCHW input -> CNHW                            in[0] = 0
+ *   CONV       EqualizedConv2d (ReplicationPad2d(pad) + conv, discriminator_9_4.py:30-40) or,
+ *              with H = W = 1 and k = 1, EqualizedLinear (discriminator_9_4.py:20-27):
+ *              y = alpha * conv(x, w) + bias; cout, k, stride, pad; w as stored [cout][cin][k][k]
+ *              (w_fwd / w_dgrad: optional GEMM-order copies, ganamd_conv_pack)
+ *   PRELU      nn.PReLU(C): per-channel slope
+ *   RESAMPLE   separable resampler (ganamd_resample2d tables: forward ri/rw/kr, adjoint
+ *              ari/arw/akr), H -> n_out (Smooth, DownSample, AdaptiveAvgPool2d(5))
+ *   PMEAN      AdaptiveAvgPool2d(1) -> [C][B]
+ *   SIGMOID    the SE gate
+ *   SCALE_ADD  y = x * s + r: x = in[0] [C][B][H][W], s = in[1] [C][B], r = in[2] (-1: none)
+ *              (discriminator_9_4.py:158-161)
+ *   MBSTD      MiniBatchStdDev(group) (discriminator_9_4.py:42-54), over `segments` equal
+ *              segments of the batch (the plan's)
+ *   FLATTEN    [C][B][H][W] -> [(c,h,w)][B] (the NCHW .view(B, -1), discriminator_9_4.py:197)
+ * The output value must be [1][B] (the critic's score).
+ *
+ * Sweeps (all on `stream`, into the caller's workspace; the plan records which values are
+ * live between calls, so forward -> backward -> tangent -> adjoint must run in that order on
+ * the SAME workspace, and the input x (and the tangent seed v) must stay valid until the
+ * adjoint has run):
+ *   forward   X_v for every value; out[b] = D(x)_b (out may be NULL)
+ *   backward  G_v = d <seed, D(x)> / d X_v (seed [B], NULL = ones); gx = G_0 (NCHW, may be NULL)
+ *   tangent   XD_v = directional derivative of X_v along the input direction v (NCHW)
+ *   adjoint   A_v  = d h / d X_v for h = <v, G_0> + <a_seed, D(x)> (a_seed may be NULL): the
+ *             reverse sweep with the second-order terms (PReLU slope, sigmoid, the SE product,
+ *             MiniBatchStdDev); ax = A_0 (NCHW, may be NULL)
+ * Parameter gradients: with `grads` non-NULL ([n_ops] entries; NULL members skip that tensor)
+ * every sweep ACCUMULATES its parameter terms into them -- backward the first-order ones,
+ * tangent the PReLU slopes' second-order term, adjoint the rest -- so backward(params) +
+ * tangent + adjoint(a_seed = w) leave d/dtheta [<w, D(x)> + <v, G_0>] in the gradient buffers.
+ *
+ * ganamd_critic_gp_step is the fused GP double-backward driver: forward, backward (seed ones),
+ * the penalty P = lambda * mean_b (||G_0,b|| - center)^2 (mode 0) or lambda * mean_b
+ * ||G_0,b||^2 (mode 1) into *penalty (device scalar), v = dP/dG_0, tangent and adjoint, with
+ * dP/dtheta accumulated into `grads`.
+ * ------------------------------------------------------------------------------------- */
+#define GANAMD_COP_SWAP 0
+#define GANAMD_COP_CONV 1
+#define GANAMD_COP_PRELU 2
+#define GANAMD_COP_RESAMPLE 3
+#define GANAMD_COP_PMEAN 4
+#define GANAMD_COP_SIGMOID 5
+#define GANAMD_COP_SCALE_ADD 6
+#define GANAMD_COP_MBSTD 7
+#define GANAMD_COP_FLATTEN 8
+
+typedef struct ganamd_critic_op {
+  int32_t kind;
+  int32_t in[3];                   /* input value ids (unused: -1); the output is value index+1 */
+  int32_t cout, k, stride, pad;    /* CONV */
+  int32_t pad_mode;                /* CONV: GANAMD_PAD_REPLICATE (EqualizedConv2d) or ZERO */
+  int32_t n_out;                   /* RESAMPLE: output side */
+  int32_t kr, akr;                 /* RESAMPLE: taps per output index (forward / adjoint table) */
+  int32_t group;                   /* MBSTD */
+  float alpha;                     /* CONV: the equalized-lr constant c */
+  const float* w;                  /* CONV weight as stored; PRELU slopes */
+  const float* w_fwd;              /* CONV: GEMM-order copies (may be NULL) */
+  const float* w_dgrad;
+  const float* bias;               /* CONV */
+  const int32_t* ri;               /* RESAMPLE forward table */
+  const float* rw;
+  const int32_t* ari;              /* RESAMPLE adjoint table */
+  const float* arw;
+} ganamd_critic_op;
+
+typedef struct ganamd_critic_grads {
+  float* gw;                       /* CONV weight / PRELU slope gradient */
+  float* gb;                       /* CONV bias gradient */
+} ganamd_critic_grads;
+
+typedef struct ganamd_critic_plan ganamd_critic_plan;
+
+/* Validates the program and sizes every value; NULL on an invalid program (shape mismatch,
+ * unknown op, a value used before it is defined).  math: GANAMD_MATH_F32 | GANAMD_MATH_BF16. */
+ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops, int B, int C0, int H0, int W0,
+                                         int segments, int math);
+void ganamd_critic_destroy(ganamd_critic_plan* plan);
+int ganamd_critic_workspace(const ganamd_critic_plan* plan, size_t* bytes);
+/* Device pointer of value v in sweep `which` (0 X, 1 G, 2 XD, 3 A) as the last sweep left it
+ * (NULL: no such value yet).  For callers that read saved activations / gradients. */
+int ganamd_critic_value(const ganamd_critic_plan* plan, int which, int v, const float** ptr);
+int ganamd_critic_forward(ganamd_critic_plan* plan, const float* x, float* out, void* workspace, hipStream_t stream);
+int ganamd_critic_backward(ganamd_critic_plan* plan, const float* seed, const ganamd_critic_grads* grads, float* gx,
+                           void* workspace, hipStream_t stream);
+int ganamd_critic_tangent(ganamd_critic_plan* plan, const float* v, const ganamd_critic_grads* grads, void* workspace,
+                          hipStream_t stream);
+int ganamd_critic_adjoint(ganamd_critic_plan* plan, const float* a_seed, const ganamd_critic_grads* grads, float* ax,
+                          void* workspace, hipStream_t stream);
+int ganamd_critic_gp_step(ganamd_critic_plan* plan, const float* x, float center, float lambda, int mode,
+                          const ganamd_critic_grads* grads, float* out, float* gx, float* norms, float* penalty,
+                          void* workspace, hipStream_t stream);
+
 /* Library identification (for load checks). */
 const char* ganamd_version(void);
 

@@ -102,3 +102,63 @@ def test_conv_block_schedule(shape, op):
             tail_cols = (geo.B * (geo.OH * geo.OW if op == 0 else 1)) - pl["nfull_t"] * pl["bn"]
             if op == 0:
                 assert n.value >= 4 * pl["S"] * geo.Cout * tail_cols
+
+
+def _critic_op(kind, ins, **kw):
+    from gan_amd import _lib
+    e = _lib.CriticOp()
+    e.kind = _lib.COP[kind]
+    for j, v in enumerate(list(ins) + [-1] * (3 - len(ins))):
+        e.ins[j] = v
+    for k, v in kw.items():
+        setattr(e, k, v)
+    return e
+
+
+def _critic_plan(ops, B=4, C0=3, H0=8, W0=8, S=1):
+    from gan_amd import _lib
+    t = (_lib.CriticOp * len(ops))(*ops)
+    return _lib.LIB.ganamd_critic_create(t, len(ops), B, C0, H0, W0, S, 0)
+
+
+def test_critic_engine_plan():
+    """The C-ABI critic engine (ganamd_critic_*) validates a program and sizes its workspace on
+    the host: a tiny critic swap -> conv 3x3 -> PReLU -> SE gate (pmean, linear, sigmoid, x*s + r)
+    -> MiniBatchStdDev -> pmean -> linear to [1][B]; malformed programs give NULL."""
+    from gan_amd import _lib
+    L = _lib.LIB
+    fake = 0x1000                   # never dereferenced by create / workspace
+    good = [_critic_op("swap", [0]),
+            _critic_op("conv", [1], cout=4, k=3, stride=1, pad=1, pad_mode=1, alpha=1.0, w=fake),    # v2 [4,B,8,8]
+            _critic_op("prelu", [2], w=fake),                                                        # v3
+            _critic_op("pmean", [3]),                                                                # v4 [4,B]
+            _critic_op("conv", [4], cout=4, k=1, stride=1, pad=0, pad_mode=0, alpha=1.0, w=fake),    # v5 linear
+            _critic_op("sigmoid", [5]),                                                              # v6
+            _critic_op("scale_add", [3, 6, 2]),                                                      # v7
+            _critic_op("mbstd", [7], group=4),                                                       # v8 [5,B,8,8]
+            _critic_op("pmean", [8]),                                                                # v9 [5,B]
+            _critic_op("conv", [9], cout=1, k=1, stride=1, pad=0, pad_mode=0, alpha=1.0, w=fake)]    # v10 [1,B]
+    p = _critic_plan(good)
+    assert p
+    n = _lib.c_size_t(0)
+    assert L.ganamd_critic_workspace(p, ctypes.byref(n)) == 0
+    # X, G, XD, A of every value at least
+    vals = [4 * 4 * 64, 4 * 4 * 64, 4 * 4, 4 * 4, 4 * 4, 4 * 4 * 64, 5 * 4 * 64, 5 * 4, 4] + [3 * 4 * 64]
+    assert n.value >= 4 * 4 * sum(vals)
+    ptr = ctypes.c_void_p()
+    assert L.ganamd_critic_value(p, 0, 3, ctypes.byref(ptr)) == 0 and not ptr.value   # nothing run yet
+    assert L.ganamd_critic_value(p, 4, 3, ctypes.byref(ptr)) == -1
+    # sweeps out of order are refused before any launch
+    assert L.ganamd_critic_backward(p, None, None, None, ctypes.c_void_p(fake), None) == -1
+    assert L.ganamd_critic_tangent(p, ctypes.c_void_p(fake), None, ctypes.c_void_p(fake), None) == -1
+    L.ganamd_critic_destroy(p)
+    bad = [
+        good[:-1] + [_critic_op("conv", [9], cout=2, k=1, pad_mode=0, alpha=1.0, stride=1, w=fake)],  # output not [1][B]
+        [_critic_op("conv", [0], cout=1, k=1, stride=1, alpha=1.0, w=fake)],                         # conv on NCHW input
+        good[:6] + [_critic_op("scale_add", [3, 2, 2])] + good[7:],                                    # gate not [C][B]
+        good[:3] + [_critic_op("pmean", [7])] + good[4:],                                              # used before defined
+        good[:1] + [_critic_op("conv", [1], cout=4, k=9, stride=1, pad=0, alpha=1.0, w=fake)] + good[2:],  # kernel > map
+    ]
+    for ops in bad:
+        assert not _critic_plan(ops)
+    assert not _critic_plan(good, B=6, S=4)          # segments must divide the batch

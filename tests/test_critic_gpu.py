@@ -266,6 +266,56 @@ def test_program_gradient_penalty_matches_autograd(gan, B):
     assert v1 <= 2 * v2 + 1e-4 and m1 <= 2 * m2 + 1e-4, (v1, m1, v2, m2)
 
 
+def test_engine_gp_step_single_call(gan):
+    """The fused GP double-backward driver as ONE C-ABI call (ganamd_critic_gp_step: forward,
+    input-gradient backward, penalty, tangent and adjoint sweeps), as a non-Python host would
+    drive it: penalty and critic parameter gradients against float64 truth at B = 4, within the
+    bars of the per-layer autograd path (train/wgangp.py:34-54, 68-69)."""
+    from gan_amd import _lib, critic, ops
+    from oracle import model as om
+    B = 4
+    P = plan()
+    D = _make_D(gan, P["d_seed"])
+    names = [n for n, _ in D.named_parameters()]
+    x = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(74))
+    xd = x.to(DEV).contiguous()
+    _zero(D)
+    run = critic.Run(critic.program_of(D), 1)
+    run._setup(xd)                                  # op table + plan + workspace (host side)
+    grads = run._grads()
+    pen = torch.zeros(1, device=DEV)
+    out = torch.empty(B, device=DEV)
+    gx = torch.empty_like(xd)
+    norms = torch.empty(B, device=DEV)
+    rc = _lib.LIB.ganamd_critic_gp_step(run.plan, xd.data_ptr(), 1.0, 10.0, 0, grads, out.data_ptr(),
+                                        gx.data_ptr(), norms.data_ptr(), pen.data_ptr(), run.ws.data_ptr(),
+                                        _lib.stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = _grads(D)
+    _zero(D)                                        # the per-layer autograd double backward
+    xi = xd.clone().requires_grad_()
+    grad, = torch.autograd.grad(D.forward_autograd(xi).sum(), xi, create_graph=True)
+    (10 * ops.grad_penalty(grad, 1.0, 1.0, 0)).backward()
+    want = _grads(D)
+    P64 = _f64_params(P)
+    x64 = x.double().requires_grad_()
+    d64 = om.discriminator(P64, x64)
+    g64, = torch.autograd.grad(d64.sum(), x64, create_graph=True)
+    n64 = g64.reshape(B, -1).pow(2).sum(1).sqrt()
+    gp64 = 10 * (n64 - 1).pow(2).mean()
+    gp64.backward()
+    truth = _f64_grads(P64, names)
+    e_pen, e_out = rel(pen[0], gp64), rel(out, d64.reshape(-1))
+    e_g, e_n = rel(gx, g64), rel(norms, n64)
+    v1, m1 = _cmp_grads(got, truth)
+    v2, m2 = _cmp_grads(want, truth)
+    print(f"gp_step: penalty {e_pen:.2e} D(x) {e_out:.2e} grad {e_g:.2e} norms {e_n:.2e}; param grads vs "
+          f"f64 vec {v1:.2e} median {m1:.2e} (autograd {v2:.2e} / {m2:.2e})")
+    assert e_out < 1e-4 and e_n < 1e-4 and e_pen < 1e-3 and e_g < 1e-3
+    assert v1 <= 2 * v2 + 1e-4 and m1 <= 2 * m2 + 1e-4, (v1, m1, v2, m2)
+
+
 def test_program_autograd_protocol(gan):
     """The drop-in keeps the reference's protocol: autograd.grad(create_graph=True) through
     D(x), then backward() of a function of that gradient -- here through the program's own

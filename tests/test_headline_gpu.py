@@ -27,7 +27,8 @@ import torch
 from oracle.params import fill_module, tensor_summary
 from tests._util import D_BAR, G_BAR, GOLDEN, check_grads, fixture, grad_norm_stats, plan, rel_err
 
-pytestmark = pytest.mark.gpu
+# host-side oracle runs of minutes each (16 threads): longer than the suite's per-test limit
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 DEV = "cuda"
 
 
