@@ -85,6 +85,7 @@ _SIGS = {
     "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
+    "ganamd_conv_wgrad2": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
     "ganamd_rowreduce_workspace": (c_size_t, [c_int, c_long]),
     "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, vp]),
     "ganamd_bn_act_fwd_seg": (c_int, [vp, c_int, c_long, c_int, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp,

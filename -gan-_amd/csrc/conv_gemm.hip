@@ -227,6 +227,11 @@ struct WgradArgs {
   float* slab;         // split-K: per-split partial weights [split][numel(out)] (null: single split)
   int out_numel;
   int bf16;
+  // two K segments (ganamd_conv_wgrad2): pixels [segK, 2 segK) read a2 / src2 (unscaled only;
+  // segK % BKW == 0 so no K-step straddles the boundary).  0: one segment.
+  const float* a2;
+  const float* src2;
+  int segK;
 };
 
 template <int BM, int BN, int WGM, int WGN>
@@ -1565,8 +1570,10 @@ void wgrad_gemm_kernel(WgradArgs p) {
     tp_kw = tp_t - tp_kh * g.KW;
   }
 
-  const rsrc_t ra_r = make_rsrc(p.a, p.a_bytes);
-  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t ra_r1 = make_rsrc(p.a, p.a_bytes);
+  const rsrc_t rx1 = make_rsrc(g.src, g.src_bytes());
+  const rsrc_t ra_r2 = make_rsrc(p.segK ? p.a2 : p.a, p.a_bytes);
+  const rsrc_t rx2 = make_rsrc(p.segK ? p.src2 : g.src, g.src_bytes());
   const rsrc_t rsa_r = make_rsrc(SCALED ? p.ascale : p.a, SCALED ? 4 * p.M * g.B : 0);
   const rsrc_t rsb_r = make_rsrc(SCALED ? g.scale : g.src, SCALED ? g.scale_bytes() : 0);
   // 16-byte A loads need 16-byte aligned rows; a quad of pixels shares its sample when ohw % 4 == 0
@@ -1587,6 +1594,11 @@ void wgrad_gemm_kernel(WgradArgs p) {
     pow_ = rr - poh * g.OW;
   }
   auto gload = [&](int kt) {
+    // segment of this K-step (uniform): the second one reads a2 / src2 at pixel n - segK
+    const bool s2 = p.segK > 0 && kt * BKW >= p.segK;
+    const rsrc_t ra_r = s2 ? ra_r2 : ra_r1;
+    const rsrc_t rx = s2 ? rx2 : rx1;
+    const int noff = s2 ? p.segK : 0, boff = s2 ? g.B : 0;
     // ---- A: rows m of gy (or x), 4 consecutive pixels per slot
     const bool full = vec_ok && (kt + 1) * BKW <= p.K;
 #pragma unroll
@@ -1596,10 +1608,11 @@ void wgrad_gemm_kernel(WgradArgs p) {
         const int m = m0 + slot / (BKW / 4), n = kt * BKW + 4 * (slot % (BKW / 4));
         const bool mok = m < p.M;
         if (full) {
-          ra[e] = bload4(ra_r, mok ? 4 * (m * p.lda + n) : kOOB);
+          ra[e] = bload4(ra_r, mok ? 4 * (m * p.lda + n - noff) : kOOB);
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[e][i] = bload(ra_r, (mok && n + i < p.K) ? 4 * (m * p.lda + n + i) : kOOB);
+          for (int i = 0; i < 4; ++i)
+            ra[e][i] = bload(ra_r, (mok && n + i < p.K) ? 4 * (m * p.lda + n - noff + i) : kOOB);
         }
         if (SCALED) {
           if (quad_b) {
@@ -1616,7 +1629,7 @@ void wgrad_gemm_kernel(WgradArgs p) {
     // ---- B: the gathered source at tap t, pixel n = kt*BKW + tk (tracked incrementally as
     // (pb, poh, pow)), channels j0 + tr + e*RSTEP
     const int n = kt * BKW + tk;
-    const int b = pb;
+    const int b = pb - boff;
     const int poh_cur = poh, pow_cur = pow_;
     const int sp = (!TP && n < p.K) ? tap_offset<MODE>(g, poh, pow_, kh, kw) : -1;
     pow_ += d_ow;
@@ -2039,7 +2052,10 @@ ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16
   conv_tile(M, &pl.bm, &pl.bn);
   // the bf16 body has 32x32 blocks only: its 48-row GEMMs run on the 64-row tile over the same
   // 48-row packed operand (rows past it read as 0 through the buffer bound, are not stored)
-  if (bf16 && pl.bm == 48) pl.bm = 64;
+  if (bf16 && pl.bm == 48) {
+    pl.bm = 64;
+    pl.bn = conv_bn(64, 0);
+  }
   if (bf16 && pl.bm == 16) pl.bm = 32;
   pl.gx = (N + pl.bn - 1) / pl.bn;
   pl.gy = (M + pl.bm - 1) / pl.bm;
@@ -2899,7 +2915,9 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
     // the modulated (scaled) variant plans the same or more splits; size for the larger
     const bool bf = d->math == GANAMD_MATH_BF16;
     const Plan a = wgrad_plan(Mw, Jw, Kpix, T, false, bf), b = wgrad_plan(Mw, Jw, Kpix, T, true, bf);
-    const int S = std::max(a.splits, b.splits);
+    // ... and for the two-segment GEMM of ganamd_conv_wgrad2 (K = 2 Kpix, unscaled)
+    const Plan c = wgrad_plan(Mw, Jw, 2 * Kpix, T, false, bf);
+    const int S = std::max(std::max(a.splits, b.splits), c.splits);
     *bytes = S > 1 ? sizeof(float) * (size_t)S * d->Cin * d->Cout * T : 0;
   } else {
     return GANAMD_EINVAL;
@@ -3140,11 +3158,8 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   return GANAMD_OK;
 }
 
-int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
-                      const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
-                      hipStream_t stream) {
-  if (!desc_ok(d) || !x || !gy || !gw) return GANAMD_EINVAL;
-  if ((x_scale == nullptr) != (gy_scale == nullptr)) return GANAMD_EINVAL;
+static WgradArgs wgrad_args(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
+                            const float* gy_scale, float alpha, float* gw, int accumulate) {
   const int T = d->KH * d->KW;
   WgradArgs p{};
   p.alpha = alpha;
@@ -3181,7 +3196,33 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
   p.out = gw;
   p.out_numel = d->Cin * d->Cout * T;
   p.accumulate = accumulate;
-  return dispatch_wgrad(p, T, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  return p;
+}
+
+int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
+                      const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
+                      hipStream_t stream) {
+  if (!desc_ok(d) || !x || !gy || !gw) return GANAMD_EINVAL;
+  if ((x_scale == nullptr) != (gy_scale == nullptr)) return GANAMD_EINVAL;
+  const WgradArgs p = wgrad_args(d, x, gy, x_scale, gy_scale, alpha, gw, accumulate);
+  return dispatch_wgrad(p, d->KH * d->KW, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK
+                                                                                                : GANAMD_ELAUNCH;
+}
+
+int ganamd_conv_wgrad2(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x2, const float* gy2,
+                       float alpha, float* gw, int accumulate, void* workspace, hipStream_t stream) {
+  if (!desc_ok(d) || !x || !gy || !x2 || !gy2 || !gw) return GANAMD_EINVAL;
+  WgradArgs p = wgrad_args(d, x, gy, nullptr, nullptr, alpha, gw, accumulate);
+  if (d->transposed || p.K % BKW != 0 || (long)2 * p.K >= (1L << 31) / 4) {   // two launches instead
+    int rc = ganamd_conv_wgrad(d, x, gy, nullptr, nullptr, alpha, gw, accumulate, workspace, stream);
+    return rc != GANAMD_OK ? rc : ganamd_conv_wgrad(d, x2, gy2, nullptr, nullptr, alpha, gw, 1, workspace, stream);
+  }
+  p.segK = p.K;
+  p.K *= 2;
+  p.a2 = gy2;
+  p.src2 = x2;
+  return dispatch_wgrad(p, d->KH * d->KW, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK
+                                                                                                : GANAMD_ELAUNCH;
 }
 
 }  // extern "C"

@@ -14,6 +14,7 @@
 //   adjoint   A_v  = d h / d X_v, h(theta) = <v, G_0(theta)> (+ <a_seed, D>): the reverse sweep
 //             carrying the second-order terms
 //               conv      A_in += W^T A_out;  dW += wgrad(X_in, A_out) + wgrad(XD_in, G_out)
+//                         (one two-segment GEMM, ganamd_conv_wgrad2)
 //               PReLU     A_in  = A_out prelu'(X);  dslope: A_out*min(X,0) here, G_out*XD[X<=0]
 //                         in the tangent sweep (ganamd_prelu_tangent)
 //               sigmoid   A_in  = A_out s(1-s) + G_out XD s(1-s)(1-2s)      (ganamd_act_adjoint)
@@ -619,10 +620,13 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
         }
         ganamd_conv_desc d = p->desc(i, false);
         const Val& yv = p->val[v];
-        if (gw && ay) TRY(ganamd_conv_wgrad(&d, x, ay, nullptr, nullptr, op.alpha, gw, 1, p->at(p->off_conv), s));
+        // dW += wgrad(X_in, A_out) + wgrad(XD_in, G_out): one GEMM over both pixel ranges
+        if (gw && ay && gy)
+          TRY(ganamd_conv_wgrad2(&d, x, ay, p->XD[u], gy, op.alpha, gw, 1, p->at(p->off_conv), s));
+        else if (gw && (ay || gy))
+          TRY(ganamd_conv_wgrad(&d, ay ? x : p->XD[u], ay ? ay : gy, nullptr, nullptr, op.alpha, gw, 1,
+                                p->at(p->off_conv), s));
         if (gb && ay) TRY(ganamd_row_dot(ay, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(p->off_rr), s));
-        if (gw && gy)
-          TRY(ganamd_conv_wgrad(&d, p->XD[u], gy, nullptr, nullptr, op.alpha, gw, 1, p->at(p->off_conv), s));
         break;
       }
       case GANAMD_COP_PRELU:

@@ -253,7 +253,7 @@ def roofline_probe(dev):
     tfile = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "roofline_traffic.json")
     if os.path.exists(tfile):
         t = json.load(open(tfile))
-        if t.get("kernel") == out["kernel"]:
+        if t.get("kernel") == out["kernel"] and t.get("batch") == out["batch"]:
             out["traffic"] = t.get("bytes_per_launch")
             out["algorithmic_bytes_per_launch"] = t.get("algorithmic_bytes")
             out["traffic_source"] = t.get("source")

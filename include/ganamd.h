@@ -132,6 +132,13 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
                       const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
                       hipStream_t stream);
 
+/* gw (+)= alpha * [dConv/dW(x, gy) + dConv/dW(x2, gy2)] as ONE GEMM over both pixel ranges (two
+ * K segments of the same weight gradient; unscaled, not transposed, else two launches).  The critic
+ * adjoint's x * a + xd * g (critic.hip; the second-order term of the gradient penalty,
+ * train/wgangp.py:68-69).  Workspace: ganamd_conv_workspace(d, GANAMD_CONV_WGRAD). */
+int ganamd_conv_wgrad2(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x2, const float* gy2,
+                       float alpha, float* gw, int accumulate, void* workspace, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Train-mode BatchNorm (1d or 2d) fused with an optional per-channel PReLU.
  * Replaces nn.BatchNorm2d/1d -> nn.PReLU pairs (generator_13_5.py:166,196,211-212,48-49,...).

@@ -737,3 +737,38 @@ def test_plane_dot_pair(ops, C, B, H):
     assert out is not None
     assert rel(out[0], (a * b1).sum((2, 3))) < 1e-5
     assert rel(out[1], (a * b2).sum((2, 3))) < 1e-5
+
+
+WGRAD2_CASES = [
+    # B, Cin, H, Cout, k, stride, pad, mode: K = B*OH*OW a multiple of 32 -> one two-segment GEMM
+    (8, 3, 64, 64, 3, 1, 1, 1),        # the critic's stem (tap-packed N)
+    (4, 64, 16, 64, 3, 1, 1, 1),
+    (4, 48, 32, 48, 5, 1, 2, 1),       # 48-row wgrad tile
+    (8, 24, 16, 20, 3, 2, 1, 1),       # strided
+    (64, 512, 1, 512, 1, 1, 0, 0),     # a linear at B = 64
+    (32, 512, 4, 512, 3, 1, 1, 1),     # the 4x4 blocks, split K
+    (4, 12, 3, 10, 3, 1, 1, 1),        # K = 36: not a whole K-step -> two launches
+]
+
+
+@pytest.mark.parametrize("case", WGRAD2_CASES)
+def test_conv_wgrad2_two_segments(ops, case):
+    """ganamd_conv_wgrad2 (the critic adjoint's x*a + xd*g, csrc/critic.hip): one GEMM over both
+    pixel ranges == the sum of the two weight gradients (float64 reference), accumulating."""
+    from gan_amd import _lib
+    B, Cin, H, Cout, k, s, p, mode = case
+    g = torch.Generator().manual_seed(7 * sum(case))
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, s, p, mode)
+    xs = [torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64) for _ in range(2)]
+    gys = [torch.randn(B, Cout, geo.OH, geo.OW, generator=g, dtype=torch.float64) for _ in range(2)]
+    w = torch.zeros(Cout, Cin, k, k, dtype=torch.float64, requires_grad=True)
+    alpha = 0.7
+    ref = sum(torch.autograd.grad(ref_conv(x, w * alpha, None, k, s, p, mode), w, gy)[0] for x, gy in zip(xs, gys))
+    gw0 = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64)
+    out = gw0.float().to(DEV)
+    ws = _lib.workspace(geo.ws_bytes(_lib.CONV_WGRAD), DEV)
+    xg, gyg = [cn(x) for x in xs], [cn(t) for t in gys]
+    rc = _lib.LIB.ganamd_conv_wgrad2(geo.desc(), _lib.ptr(xg[0]), _lib.ptr(gyg[0]), _lib.ptr(xg[1]), _lib.ptr(gyg[1]),
+                                     alpha, _lib.ptr(out), 1, _lib.ptr(ws), _lib.stream())
+    assert rc == 0
+    assert rel(out, gw0 + ref) < 1e-5

@@ -11,22 +11,27 @@ import csv
 import gzip
 import sys
 
-PROBES = [  # (kernel name as rocprof prints it, grid blocks, algorithmic GFLOP per launch, label)
-    ("conv_gemm_kernel<96, 128, 1, 4, 1, true, false>", 2048, 2.0 * 64 * 64 * 64 * 96 * 96 * 25 / 1e9,
-     "dominant: G13_5 modulated conv fwd B=64 96->96 5x5 64x64"),
-    ("conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", 768, 2.0 * 96 * 32 * 32 * 128 * 128 * 9 / 1e9,
-     "critic probe: D9_4 conv fwd B=96 128->128 3x3 32x32"),
+PROBES = [  # (kernel name as rocprof prints it, batch per launched block, GFLOP per image, label); the probe
+    # batch is the whole-tile batch bench.py picks at run time (_whole_tile_geo), read back from the grid
+    ("conv_gemm_kernel<96, 128, 1, 4, 1, true, false>", 128 / (64 * 64), 2.0 * 64 * 64 * 96 * 96 * 25 / 1e9,
+     "dominant: G13_5 modulated conv fwd 96->96 5x5 64x64"),
+    ("conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", 128 / (32 * 32), 2.0 * 32 * 32 * 128 * 128 * 9 / 1e9,
+     "critic probe: D9_4 conv fwd 128->128 3x3 32x32"),
 ]
 PEAK = 157.3
 
 path = sys.argv[1]
 rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-for kernel, blocks, gflop, label in PROBES:
+for kernel, per_block, gflop_img, label in PROBES:
     best, run = [], []
     for r in rows:
-        if kernel in r["Kernel_Name"] and int(r["Grid_Size_X"]) == blocks * 256:
+        if kernel in r["Kernel_Name"] and (not run or r["Grid_Size_X"] == run[0]["Grid_Size_X"]):
             run.append(r)
+        elif kernel in r["Kernel_Name"]:
+            if len(run) > len(best):
+                best = run
+            run = [r]
         else:
             if len(run) > len(best):
                 best = run
@@ -34,10 +39,13 @@ for kernel, blocks, gflop, label in PROBES:
     if len(run) > len(best):
         best = run
     if len(best) < 20:
-        print(f"{label}: no run of >= 20 consecutive launches of {kernel} at {blocks} blocks")
+        print(f"{label}: no run of >= 20 consecutive launches of {kernel}")
         continue
+    blocks = int(best[0]["Grid_Size_X"]) // 256
+    B = round(blocks * per_block)
+    gflop = gflop_img * B
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in best[3:]]
     avg = sum(d) / len(d)
-    print(f"{label}: {kernel} at {blocks} blocks, {len(d)} launches (run of {len(best)}, first 3 skipped)")
+    print(f"{label}: {kernel} at {blocks} blocks (B={B}), {len(d)} launches (run of {len(best)}, first 3 skipped)")
     print(f"  average {avg:.1f} us  min {min(d):.1f}  max {max(d):.1f}  -> {gflop / avg * 1e-3 * 1e3:.1f} TF/s "
           f"({gflop:.2f} GFLOP per launch), {gflop / avg * 1e3 / PEAK:.3f} of {PEAK}")
