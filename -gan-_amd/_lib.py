@@ -129,6 +129,8 @@ _SIGS = {
     "ganamd_critic_destroy": (None, [vp]),
     "ganamd_critic_workspace": (c_int, [vp, ctypes.POINTER(c_size_t)]),
     "ganamd_critic_value": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ganamd_critic_region_bytes": (c_int, [vp, c_int, ctypes.POINTER(c_size_t)]),
+    "ganamd_critic_bind": (c_int, [vp, c_int, vp]),
     "ganamd_critic_forward": (c_int, [vp, vp, vp, vp, vp]),
     "ganamd_critic_backward": (c_int, [vp, vp, vp, vp, vp, vp]),
     "ganamd_critic_tangent": (c_int, [vp, vp, vp, vp, vp]),

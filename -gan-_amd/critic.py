@@ -248,11 +248,14 @@ class _Values:
         if v == 0:
             return run.x if self.which == 0 else run.v
         C, H, W = run.sh[v]
-        off = (p.value - run.ws.data_ptr()) // 4
         n = C * run.B * H * W
-        if off < 0 or off + n > run.ws.numel():
+        for reg in run.regions:
+            off = (p.value - reg.data_ptr()) // 4 if reg is not None else -1
+            if 0 <= off and off + n <= reg.numel():
+                t = reg[off:off + n]
+                break
+        else:
             raise _lib.GanAmdError(f"critic value {v} outside the run's workspace")
-        t = run.ws[off:off + n]
         # per-sample vectors (linear / pool / flatten outputs and activations of them) are [C, B];
         # maps (a 1x1 conv output included) [C, B, H, W]
         return t.view(C, run.B) if run.vec[v] else t.view(C, run.B, H, W)
@@ -266,14 +269,16 @@ class _Values:
 
 class Run:
     """One critic evaluation through the C-ABI engine (ganamd_critic_*): the plan of the program
-    at this batch, the workspace holding every saved activation, gradient, tangent and adjoint,
-    and the sweeps.  ``X`` / ``G`` / ``XD`` read values back (tests, tools)."""
+    at this batch, the workspace regions holding the saved activations (X), gradients (G),
+    tangents (XD) and adjoints (A) -- each allocated when the sweep that fills it starts, so a
+    first-order evaluation holds X and G only -- and the sweeps.  ``X`` / ``G`` / ``XD`` read
+    values back (tests, tools)."""
 
     def __init__(self, prog: Program, segments: int = 1):
         self.prog = prog
         self.segments = segments
         self.plan = None
-        self.ws = None
+        self.regions = [None] * 4       # scratch + X, G, XD, A: allocated by the sweep that fills them
         self.keep = []
         self.x = self.v = None
         self.X, self.G, self.XD = _Values(self, 0), _Values(self, 1), _Values(self, 2)
@@ -295,9 +300,15 @@ class Run:
         self.plan = LIB.ganamd_critic_create(self.table, len(self.prog.ops), B, C, H, W, self.segments, ops._MATH[0])
         if not self.plan:
             raise _lib.GanAmdError(f"critic program rejected by ganamd_critic_create (B={B}, segments={self.segments})")
-        n = _lib.c_size_t(0)
-        check(LIB.ganamd_critic_workspace(self.plan, _lib.ctypes.byref(n)), "critic_workspace")
-        self.ws = workspace(n.value, x.device)
+        self._region(0, x.device)
+
+    def _region(self, which, device):
+        """Allocate and bind workspace region ``which`` (ganamd_critic_region_bytes / _bind)."""
+        if self.regions[which] is None:
+            n = _lib.c_size_t(0)
+            check(LIB.ganamd_critic_region_bytes(self.plan, which, _lib.ctypes.byref(n)), "critic_region_bytes")
+            self.regions[which] = workspace(n.value, device)
+            check(LIB.ganamd_critic_bind(self.plan, which, ptr(self.regions[which])), "critic_bind")
 
     def _grads(self):
         """ganamd_critic_grads[] of the parameters that want a gradient (created as zeros)."""
@@ -345,7 +356,7 @@ class Run:
         self.x = x_nchw
         self._setup(x_nchw)
         self._count("forward")
-        check(LIB.ganamd_critic_forward(self.plan, ptr(x_nchw), None, ptr(self.ws), stream()), "critic_forward")
+        check(LIB.ganamd_critic_forward(self.plan, ptr(x_nchw), None, None, stream()), "critic_forward")
         return self.X[self.prog.out].clone()               # [1, B], not a view of the workspace
 
     def backward(self, seed, params: bool, need_input: bool):
@@ -354,8 +365,9 @@ class Run:
         self._count("backward", params, need_input)
         self.seed = seed.contiguous()
         gx = torch.empty_like(self.x) if need_input else None
+        self._region(1, self.x.device)
         check(LIB.ganamd_critic_backward(self.plan, ptr(self.seed), self._grads() if params else None, ptr(gx),
-                                         ptr(self.ws), stream()), "critic_backward")
+                                         None, stream()), "critic_backward")
         return gx
 
     def tangent(self, v_nchw, params: bool):
@@ -363,7 +375,8 @@ class Run:
         their gradients when ``params``."""
         self._count("tangent")
         self.v = v_nchw.contiguous()
-        check(LIB.ganamd_critic_tangent(self.plan, ptr(self.v), self._grads() if params else None, ptr(self.ws),
+        self._region(2, self.x.device)
+        check(LIB.ganamd_critic_tangent(self.plan, ptr(self.v), self._grads() if params else None, None,
                                         stream()), "critic_tangent")
         return self.XD[self.prog.out]
 
@@ -373,8 +386,9 @@ class Run:
         self._count("adjoint", params, need_input, seeded=a_seed is not None)
         self.a_seed = None if a_seed is None else a_seed.contiguous()
         ax = torch.empty_like(self.x) if need_input else None
+        self._region(3, self.x.device)
         check(LIB.ganamd_critic_adjoint(self.plan, ptr(self.a_seed), self._grads() if params else None, ptr(ax),
-                                        ptr(self.ws), stream()), "critic_adjoint")
+                                        None, stream()), "critic_adjoint")
         return ax
 
 # ------------------------------------------------------------------------------------------

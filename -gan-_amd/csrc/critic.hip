@@ -33,6 +33,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "../../include/ganamd.h"
@@ -81,6 +83,29 @@ int fill(float* p, long n, float v, hipStream_t s) {
   return ok(hipGetLastError());
 }
 
+// Weight gradients off the critical path: inside a backward / adjoint sweep every conv's weight
+// (and bias) gradient is forked onto a side stream -- it needs only the conv's saved input and its
+// output gradient, while the sweep's chain continues with the input gradient -- and the sweep joins
+// it at its end.  Under graph capture the fork / join become graph edges.  One side stream per
+// device (created on first use); each plan has its own fork / join events.  Same kernels, same
+// per-buffer accumulation order (all weight gradients of a sweep run in sweep order on the side
+// stream), so results are unchanged.  GANAMD_CRITIC_SIDE=0 keeps everything on the caller's stream.
+hipStream_t side_stream() {
+  static std::mutex mu;
+  static hipStream_t streams[64] = {};
+  static const bool on = [] {
+    const char* v = getenv("GANAMD_CRITIC_SIDE");
+    return !v || atoi(v) != 0;
+  }();
+  if (!on) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
+    streams[dev] = nullptr;
+  return streams[dev];
+}
+
 struct Val {
   int C = 0, H = 0, W = 0;
   long n = 0;          // C * B * H * W
@@ -109,14 +134,25 @@ struct ganamd_critic_plan {
   // workspace layout (bytes), set by ganamd_critic_workspace
   bool sized = false;
   size_t total = 0, off_tmp = 0, off_conv = 0, off_rr = 0, off_mb = 0, off_gp = 0, off_ones = 0, off_v = 0,
-         off_g0 = 0, off_norms = 0;
+         off_g0 = 0, off_norms = 0, off_conv2 = 0, off_rr2 = 0;   // *2: the side stream's scratch
   size_t conv_ws = 0, rr_ws = 0, mb_ws = 0, gp_ws = 0;
-  std::vector<size_t> offX, offG, offXD, offA;
-  // state between sweeps
+  std::vector<size_t> offX, offG, offXD, offA;   // X: in region 0 after the scratch; G, XD, A: regions 1-3
+  size_t rsz[4] = {0, 0, 0, 0};                  // region bytes
+  // state between sweeps: the regions' bases -- carved from one contiguous workspace (ws != NULL)
+  // or bound one by one (ganamd_critic_bind, ws == NULL)
   char* ws = nullptr;
+  char* R[4] = {nullptr, nullptr, nullptr, nullptr};
   int stage = 0;                   // 1 forward, 2 backward, 3 tangent done
   std::vector<float*> X, XD;
   Sweep G, A;
+  // weight-gradient side stream (see side_stream) and this plan's fork / join events
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool forked = false;
+  ~ganamd_critic_plan() {
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+  }
 
   ganamd_conv_desc desc(int i, bool packed) const {
     const ganamd_critic_op& op = ops[i];
@@ -139,7 +175,8 @@ struct ganamd_critic_plan {
     d.math = math;
     return d;
   }
-  float* at(size_t off) const { return reinterpret_cast<float*>(ws + off); }
+  float* at(size_t off) const { return reinterpret_cast<float*>(R[0] + off); }   // scratch and X
+  float* atr(int r, size_t off) const { return reinterpret_cast<float*>(R[r] + off); }
 };
 
 namespace {
@@ -215,10 +252,43 @@ int resample(const Plan& p, const ganamd_critic_op& op, const Val& x, const floa
 const float* wf(const ganamd_critic_op& op) { return op.w_fwd ? op.w_fwd : op.w; }
 const float* wd(const ganamd_critic_op& op) { return op.w_dgrad ? op.w_dgrad : op.w; }
 
+// need_stage: 0 forward, 1 backward, 2 tangent, 3 adjoint (the sweep that must have run before,
+// and the regions the sweep touches: 0..need_stage)
 int check_ws(Plan& p, void* ws, int need_stage) {
-  if (!p.sized || !ws) return GANAMD_EINVAL;
-  if (need_stage > 0 && (p.stage < need_stage || p.ws != ws)) return GANAMD_EINVAL;
+  if (!p.sized) return GANAMD_EINVAL;
+  if (ws) {
+    if (need_stage == 0) {                 // one contiguous workspace: carve the four regions
+      p.ws = static_cast<char*>(ws);
+      size_t o = 0;
+      for (int r = 0; r < 4; ++r) {
+        p.R[r] = p.ws + o;
+        o += p.rsz[r];
+      }
+    } else if (p.ws != ws) {
+      return GANAMD_EINVAL;
+    }
+  } else {
+    if (need_stage == 0) p.ws = nullptr;
+    if (p.ws) return GANAMD_EINVAL;        // started contiguous: stays contiguous
+    for (int r = 0; r <= need_stage; ++r)
+      if (!p.R[r]) return GANAMD_EINVAL;
+  }
+  if (need_stage > 0 && p.stage < need_stage) return GANAMD_EINVAL;
   return GANAMD_OK;
+}
+
+// the stream a weight gradient goes to: the side stream (after a fork from s) or s itself
+hipStream_t wstream(Plan& p, hipStream_t s) {
+  if (!p.side) return s;
+  if (hipEventRecord(p.ev_fork, s) != hipSuccess || hipStreamWaitEvent(p.side, p.ev_fork, 0) != hipSuccess) return s;
+  p.forked = true;
+  return p.side;
+}
+int join(Plan& p, hipStream_t s) {
+  if (!p.forked) return GANAMD_OK;
+  p.forked = false;
+  if (hipEventRecord(p.ev_join, p.side) != hipSuccess) return GANAMD_ELAUNCH;
+  return ok(hipStreamWaitEvent(s, p.ev_join, 0));
 }
 
 #define TRY(expr)                       \
@@ -321,6 +391,10 @@ ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops,
     S->own.assign(nv, nullptr);
     S->borrowed.assign(nv, 0);
   }
+  p->side = side_stream();
+  if (p->side && (hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                  hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess))
+    p->side = nullptr;                                   // sequential on the caller's stream
   return p;
 }
 
@@ -368,26 +442,51 @@ int ganamd_critic_workspace(const ganamd_critic_plan* cplan, size_t* bytes) {
     p->offG.assign(nv, 0);
     p->offXD.assign(nv, 0);
     p->offA.assign(nv, 0);
-    for (int v = 1; v < nv; ++v) {
-      const size_t nb = p->val[v].n * sizeof(float);
-      p->offX[v] = take(nb);
-      p->offG[v] = take(nb);
-      p->offXD[v] = take(nb);
-      p->offA[v] = take(nb);
-    }
+    // region 0: scratch, then X
     p->off_tmp = take(p->maxn * sizeof(float));
     p->off_conv = take(conv);
     p->off_rr = take(rr);
+    p->off_conv2 = take(conv);
+    p->off_rr2 = take(rr);
     p->off_mb = take(p->mb_ws);
     p->off_gp = take(p->gp_ws);
     p->off_ones = take(std::max(p->B, 1) * sizeof(float));
     p->off_v = take(p->val[0].n * sizeof(float));
     p->off_g0 = take(p->val[0].n * sizeof(float));
     p->off_norms = take(p->B * sizeof(float));
-    p->total = off;
+    for (int v = 1; v < nv; ++v) p->offX[v] = take(p->val[v].n * sizeof(float));
+    p->rsz[0] = off;
+    std::vector<size_t>* offs[3] = {&p->offG, &p->offXD, &p->offA};
+    for (int r = 1; r < 4; ++r) {
+      off = 0;
+      for (int v = 1; v < nv; ++v) (*offs[r - 1])[v] = take(p->val[v].n * sizeof(float));
+      p->rsz[r] = off;
+    }
+    p->total = p->rsz[0] + p->rsz[1] + p->rsz[2] + p->rsz[3];
     p->sized = true;
   }
   *bytes = p->total;
+  return GANAMD_OK;
+}
+
+int ganamd_critic_region_bytes(const ganamd_critic_plan* p, int which, size_t* bytes) {
+  size_t total = 0;
+  if (!p || !bytes || which < 0 || which > 3) return GANAMD_EINVAL;
+  TRY(ganamd_critic_workspace(p, &total));
+  *bytes = p->rsz[which];
+  return GANAMD_OK;
+}
+
+int ganamd_critic_bind(ganamd_critic_plan* p, int which, void* region) {
+  if (!p || !region || which < 0 || which > 3 || !p->sized) return GANAMD_EINVAL;
+  if (which == 0) {                         // a new evaluation in bound mode
+    p->ws = nullptr;
+    for (char*& r : p->R) r = nullptr;
+    p->stage = 0;
+  } else if (p->ws) {
+    return GANAMD_EINVAL;                   // the plan runs on a contiguous workspace
+  }
+  p->R[which] = static_cast<char*>(region);
   return GANAMD_OK;
 }
 
@@ -401,13 +500,8 @@ int ganamd_critic_value(const ganamd_critic_plan* p, int which, int v, const flo
 int ganamd_critic_forward(ganamd_critic_plan* p, const float* x, float* out, void* workspace, hipStream_t s) {
   if (!p || !x) return GANAMD_EINVAL;
   TRY(check_ws(*p, workspace, 0));
-  p->ws = static_cast<char*>(workspace);
   p->stage = 0;
   p->X[0] = const_cast<float*>(x);
-  for (int v = 1; v < (int)p->val.size(); ++v) {
-    p->G.own[v] = p->at(p->offG[v]);
-    p->A.own[v] = p->at(p->offA[v]);
-  }
   for (int i = 0; i < (int)p->ops.size(); ++i) {
     const ganamd_critic_op& op = p->ops[i];
     const int v = i + 1;
@@ -451,6 +545,7 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
   TRY(check_ws(*p, workspace, 1));
   Sweep& G = p->G;
   G.reset();
+  for (int v = 1; v < (int)p->val.size(); ++v) G.own[v] = p->atr(1, p->offG[v]);
   if (!seed) {
     float* ones = p->at(p->off_ones);
     TRY(fill(ones, p->B, 1.f, s));
@@ -481,11 +576,16 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
           }, s));
         }
         const Val& yv = p->val[v];
-        if (gw) {
-          ganamd_conv_desc d = p->desc(i, false);
-          TRY(ganamd_conv_wgrad(&d, x, gy, nullptr, nullptr, op.alpha, gw, 1, p->at(p->off_conv), s));
+        if (gw || gb) {
+          const hipStream_t ws = wstream(*p, s);
+          const bool sd = ws != s;
+          if (gw) {
+            ganamd_conv_desc d = p->desc(i, false);
+            TRY(ganamd_conv_wgrad(&d, x, gy, nullptr, nullptr, op.alpha, gw, 1, p->at(sd ? p->off_conv2 : p->off_conv),
+                                  ws));
+          }
+          if (gb) TRY(ganamd_row_dot(gy, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(sd ? p->off_rr2 : p->off_rr), ws));
         }
-        if (gb) TRY(ganamd_row_dot(gy, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(p->off_rr), s));
         break;
       }
       case GANAMD_COP_PRELU:
@@ -533,6 +633,7 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
         break;
     }
   }
+  TRY(join(*p, s));
   p->stage = 2;
   return GANAMD_OK;
 }
@@ -548,7 +649,7 @@ int ganamd_critic_tangent(ganamd_critic_plan* p, const float* vdir, const ganamd
     const Val& xv = p->val[op.in[0]];
     const float* xd = p->XD[op.in[0]];
     const float* x = p->X[op.in[0]];
-    float* y = p->at(p->offXD[v]);
+    float* y = p->atr(2, p->offXD[v]);
     const long L = (long)p->B * xv.hw();
     switch (op.kind) {
       case GANAMD_COP_SWAP: TRY(swap_in(*p, xd, y, s)); break;
@@ -592,6 +693,7 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
   TRY(check_ws(*p, workspace, 3));
   Sweep& A = p->A;
   A.reset();
+  for (int v = 1; v < (int)p->val.size(); ++v) A.own[v] = p->atr(3, p->offA[v]);
   if (a_seed) {
     A.cur[p->out] = const_cast<float*>(a_seed);
     A.borrowed[p->out] = 1;
@@ -621,12 +723,17 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
         ganamd_conv_desc d = p->desc(i, false);
         const Val& yv = p->val[v];
         // dW += wgrad(X_in, A_out) + wgrad(XD_in, G_out): one GEMM over both pixel ranges
-        if (gw && ay && gy)
-          TRY(ganamd_conv_wgrad2(&d, x, ay, p->XD[u], gy, op.alpha, gw, 1, p->at(p->off_conv), s));
-        else if (gw && (ay || gy))
-          TRY(ganamd_conv_wgrad(&d, ay ? x : p->XD[u], ay ? ay : gy, nullptr, nullptr, op.alpha, gw, 1,
-                                p->at(p->off_conv), s));
-        if (gb && ay) TRY(ganamd_row_dot(ay, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(p->off_rr), s));
+        if ((gw && (ay || gy)) || (gb && ay)) {
+          const hipStream_t ws = wstream(*p, s);
+          float* cw = p->at(ws != s ? p->off_conv2 : p->off_conv);
+          if (gw && ay && gy)
+            TRY(ganamd_conv_wgrad2(&d, x, ay, p->XD[u], gy, op.alpha, gw, 1, cw, ws));
+          else if (gw)
+            TRY(ganamd_conv_wgrad(&d, ay ? x : p->XD[u], ay ? ay : gy, nullptr, nullptr, op.alpha, gw, 1, cw, ws));
+          if (gb && ay)
+            TRY(ganamd_row_dot(ay, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(ws != s ? p->off_rr2 : p->off_rr),
+                               ws));
+        }
         break;
       }
       case GANAMD_COP_PRELU:
@@ -711,7 +818,7 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
         break;
     }
   }
-  return GANAMD_OK;
+  return join(*p, s);
 }
 
 int ganamd_critic_gp_step(ganamd_critic_plan* p, const float* x, float center, float lambda, int mode,

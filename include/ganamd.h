@@ -488,6 +488,14 @@ ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops,
                                          int segments, int math);
 void ganamd_critic_destroy(ganamd_critic_plan* plan);
 int ganamd_critic_workspace(const ganamd_critic_plan* plan, size_t* bytes);
+/* The workspace in four regions, each allocated only when the sweep that fills it starts:
+ * 0 = scratch + X (forward), 1 = G (backward), 2 = XD (tangent), 3 = A (adjoint).  With
+ * `workspace` = NULL every sweep uses the regions bound here (binding region 0 starts a new
+ * evaluation); with a non-NULL `workspace` (ganamd_critic_workspace bytes) the four regions are
+ * carved from it in that order.  A first-order evaluation (the real / fake critic passes) then
+ * needs regions 0-1 only. */
+int ganamd_critic_region_bytes(const ganamd_critic_plan* plan, int which, size_t* bytes);
+int ganamd_critic_bind(ganamd_critic_plan* plan, int which, void* region);
 /* Device pointer of value v in sweep `which` (0 X, 1 G, 2 XD, 3 A) as the last sweep left it
  * (NULL: no such value yet).  For callers that read saved activations / gradients. */
 int ganamd_critic_value(const ganamd_critic_plan* plan, int which, int v, const float** ptr);

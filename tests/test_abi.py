@@ -145,6 +145,15 @@ def test_critic_engine_plan():
     # X, G, XD, A of every value at least
     vals = [4 * 4 * 64, 4 * 4 * 64, 4 * 4, 4 * 4, 4 * 4, 4 * 4 * 64, 5 * 4 * 64, 5 * 4, 4] + [3 * 4 * 64]
     assert n.value >= 4 * 4 * sum(vals)
+    regions = []
+    for r in range(4):
+        b = _lib.c_size_t(0)
+        assert L.ganamd_critic_region_bytes(p, r, ctypes.byref(b)) == 0
+        regions.append(b.value)
+    assert sum(regions) == n.value and regions[1] == regions[2] == regions[3] >= 4 * sum(vals[:-1])
+    assert L.ganamd_critic_bind(p, 1, ctypes.c_void_p(fake)) == 0
+    # a sweep whose regions are not all bound is refused before any launch
+    assert L.ganamd_critic_forward(p, ctypes.c_void_p(fake), None, None, None) == -1
     ptr = ctypes.c_void_p()
     assert L.ganamd_critic_value(p, 0, 3, ctypes.byref(ptr)) == 0 and not ptr.value   # nothing run yet
     assert L.ganamd_critic_value(p, 4, 3, ctypes.byref(ptr)) == -1

@@ -271,6 +271,7 @@ def test_engine_gp_step_single_call(gan):
     input-gradient backward, penalty, tangent and adjoint sweeps), as a non-Python host would
     drive it: penalty and critic parameter gradients against float64 truth at B = 4, within the
     bars of the per-layer autograd path (train/wgangp.py:34-54, 68-69)."""
+    import ctypes
     from gan_amd import _lib, critic, ops
     from oracle import model as om
     B = 4
@@ -281,14 +282,17 @@ def test_engine_gp_step_single_call(gan):
     xd = x.to(DEV).contiguous()
     _zero(D)
     run = critic.Run(critic.program_of(D), 1)
-    run._setup(xd)                                  # op table + plan + workspace (host side)
+    run._setup(xd)                                  # op table + plan (host side)
     grads = run._grads()
+    nbytes = _lib.c_size_t(0)                       # one contiguous workspace, as a C host would use
+    assert _lib.LIB.ganamd_critic_workspace(run.plan, ctypes.byref(nbytes)) == 0
+    ws = _lib.workspace(nbytes.value, DEV)
     pen = torch.zeros(1, device=DEV)
     out = torch.empty(B, device=DEV)
     gx = torch.empty_like(xd)
     norms = torch.empty(B, device=DEV)
     rc = _lib.LIB.ganamd_critic_gp_step(run.plan, xd.data_ptr(), 1.0, 10.0, 0, grads, out.data_ptr(),
-                                        gx.data_ptr(), norms.data_ptr(), pen.data_ptr(), run.ws.data_ptr(),
+                                        gx.data_ptr(), norms.data_ptr(), pen.data_ptr(), ws.data_ptr(),
                                         _lib.stream())
     assert rc == 0
     torch.cuda.synchronize()
