@@ -47,5 +47,5 @@ for kernel, per_block, gflop_img, label in PROBES:
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in best[3:]]
     avg = sum(d) / len(d)
     print(f"{label}: {kernel} at {blocks} blocks (B={B}), {len(d)} launches (run of {len(best)}, first 3 skipped)")
-    print(f"  average {avg:.1f} us  min {min(d):.1f}  max {max(d):.1f}  -> {gflop / avg * 1e-3 * 1e3:.1f} TF/s "
+    print(f"  average {avg:.1f} us  min {min(d):.1f}  max {max(d):.1f}  -> {gflop / avg * 1e3:.1f} TF/s "
           f"({gflop:.2f} GFLOP per launch), {gflop / avg * 1e3 / PEAK:.3f} of {PEAK}")
