@@ -10,7 +10,9 @@ Changed: the reference pickles whole modules and, on l
 the loaded network).  Here ``generator`` / ``discriminator`` are ``state_dict()``s keyed by the
 reference's own parameter/buffer names (drop-in and reference modules load each other's), they
 are loaded IN PLACE (the flat-buffer views and the optimizers stay bound), and the optimizer
-moments and step counters are saved too.  Everything is tensors/str/int, so
+moments and step counters are saved too, and so are the device RNG's stream offsets
+(``DeviceRNG.state()``: z / noise, eps and synthetic-data streams), so a resumed run continues the
+random sequence instead of redrawing the first run's numbers.  Everything is tensors/str/int, so
 ``torch.load(..., weights_only=True)`` reads it.
 """
 from __future__ import annotations
@@ -50,13 +52,26 @@ class CheckpointMixin:
                  "discriminator": _cpu_state(self.discriminator), "discriminator_name": self.discriminator_name,
                  "method": train_name, "epoch": e, "i": ii,
                  "optimizer_G": self.optimizer_G.state_dict(), "optimizer_D": self.optimizer_D.state_dict()}
+        rng = getattr(self, "rng", None)
+        if hasattr(rng, "state"):
+            state["rng"] = {str(k): v.detach().to("cpu") for k, v in rng.state().items()}
         path = ckpt_path(self.ckpt_root, self.generator_name, self.discriminator_name, train_name, e, ii)
+        err = None
         if not _is_dist() or torch.distributed.get_rank() == 0:
             # data parallel: the replicas are identical, rank 0 writes the file
-            os.makedirs(self.ckpt_root, exist_ok=True)
-            torch.save(state, path)
+            try:
+                os.makedirs(self.ckpt_root, exist_ok=True)
+                torch.save(state, path)
+            except Exception as ex:          # noqa: BLE001 -- every rank learns of it below
+                err = ex
         if _is_dist():
-            torch.distributed.barrier()     # no rank returns the path before the file is complete
+            # no rank returns before the file is complete, and every rank sees rank 0's failure
+            flag = [None if err is None else f"{type(err).__name__}: {err}"]
+            torch.distributed.broadcast_object_list(flag, src=0)
+            if flag[0] is not None and err is None:
+                raise RuntimeError(f"checkpoint save failed on rank 0: {flag[0]}")
+        if err is not None:
+            raise err
         return path
 
     def _load(self, name):
@@ -81,6 +96,9 @@ class CheckpointMixin:
         if "optimizer_G" in ck:
             self.optimizer_G.load_state_dict(ck["optimizer_G"])
         self.epoch, self.i = int(ck["epoch"]), int(ck["i"])
+        rng = getattr(self, "rng", None)
+        if "rng" in ck and hasattr(rng, "set_state"):
+            rng.set_state({int(k): v for k, v in ck["rng"].items()})
         return True
 
     def load_discriminator_ckpt(self, name):

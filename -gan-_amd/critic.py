@@ -290,6 +290,11 @@ class Run:
 
     def _setup(self, x):
         B, C, H, W = x.shape
+        if self.plan:                   # a new evaluation on this Run: nothing of the old one is reused
+            LIB.ganamd_critic_destroy(self.plan)
+            self.plan = None
+            self.regions = [None] * 4
+            self.keep = []
         self.B = B
         self.sh = _shapes(self.prog, C, H, W)
         self.vec = {0: False}

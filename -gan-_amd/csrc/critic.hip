@@ -86,24 +86,29 @@ int fill(float* p, long n, float v, hipStream_t s) {
 // Weight gradients off the critical path: inside a backward / adjoint sweep every conv's weight
 // (and bias) gradient is forked onto a side stream -- it needs only the conv's saved input and its
 // output gradient, while the sweep's chain continues with the input gradient -- and the sweep joins
-// it at its end.  Under graph capture the fork / join become graph edges.  One side stream per
-// device (created on first use); each plan has its own fork / join events.  Same kernels, same
-// per-buffer accumulation order (all weight gradients of a sweep run in sweep order on the side
-// stream), so results are unchanged.  GANAMD_CRITIC_SIDE=0 keeps everything on the caller's stream.
-hipStream_t side_stream() {
+// it at its end.  Under graph capture the fork / join become graph edges.  The side stream belongs
+// to the CALLER's stream (one per (device, caller stream), created on first use, never shared
+// between two caller streams): two plans driven from two threads on two streams never serialise
+// on one side stream, and a capture on one caller stream pulls only that stream's side stream into
+// its graph -- an eager sweep on another stream never touches a stream being captured.  Each plan
+// has its own fork / join events.  Same kernels, same per-buffer accumulation order (all weight
+// gradients of a sweep run in sweep order on the side stream), so results are unchanged.
+hipStream_t side_stream(hipStream_t caller) {
+  struct Entry {
+    int dev;
+    hipStream_t caller, side;
+  };
   static std::mutex mu;
-  static hipStream_t streams[64] = {};
-  static const bool on = [] {
-    const char* v = getenv("GANAMD_CRITIC_SIDE");
-    return !v || atoi(v) != 0;
-  }();
-  if (!on) return nullptr;
+  static std::vector<Entry> table;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
-  if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
-    streams[dev] = nullptr;
-  return streams[dev];
+  for (const Entry& e : table)
+    if (e.dev == dev && e.caller == caller) return e.side;
+  hipStream_t side = nullptr;
+  if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  table.push_back(Entry{dev, caller, side});
+  return side;
 }
 
 struct Val {
@@ -145,10 +150,11 @@ struct ganamd_critic_plan {
   int stage = 0;                   // 1 forward, 2 backward, 3 tangent done
   std::vector<float*> X, XD;
   Sweep G, A;
-  // weight-gradient side stream (see side_stream) and this plan's fork / join events
+  // this plan's fork / join events to the caller stream's side stream (see side_stream); `side`
+  // is the side stream of the sweep in progress
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool forked = false;
+  bool forked = false, has_events = false;
   ~ganamd_critic_plan() {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
@@ -278,11 +284,15 @@ int check_ws(Plan& p, void* ws, int need_stage) {
 }
 
 // the stream a weight gradient goes to: the side stream (after a fork from s) or s itself
+// (every call forks again: the weight gradient needs the output gradient the sweep has just made)
 hipStream_t wstream(Plan& p, hipStream_t s) {
-  if (!p.side) return s;
-  if (hipEventRecord(p.ev_fork, s) != hipSuccess || hipStreamWaitEvent(p.side, p.ev_fork, 0) != hipSuccess) return s;
+  if (!p.has_events) return s;
+  hipStream_t side = p.forked ? p.side : side_stream(s);
+  if (!side) return s;
+  if (hipEventRecord(p.ev_fork, s) != hipSuccess || hipStreamWaitEvent(side, p.ev_fork, 0) != hipSuccess) return s;
+  p.side = side;
   p.forked = true;
-  return p.side;
+  return side;
 }
 int join(Plan& p, hipStream_t s) {
   if (!p.forked) return GANAMD_OK;
@@ -391,10 +401,8 @@ ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops,
     S->own.assign(nv, nullptr);
     S->borrowed.assign(nv, 0);
   }
-  p->side = side_stream();
-  if (p->side && (hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
-                  hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess))
-    p->side = nullptr;                                   // sequential on the caller's stream
+  p->has_events = hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) == hipSuccess;   // else: sequential
   return p;
 }
 

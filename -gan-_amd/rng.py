@@ -87,9 +87,14 @@ class DeviceRNG:
         return {s: r.offset.clone() for s, r in [(self.stream, self)] + [(f.stream, f) for f in self._forks.values()]}
 
     def set_state(self, st):
+        """Restore offsets saved by state() (forks missing here are created)."""
         self.offset.copy_(st[self.stream])
+        for s in st:
+            if s != self.stream:
+                self.fork(s - self.stream)
         for f in self._forks.values():
-            f.offset.copy_(st[f.stream])
+            if f.stream in st:
+                f.offset.copy_(st[f.stream])
 
 
 class ReplayRNG:

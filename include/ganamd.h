@@ -445,6 +445,13 @@ int ganamd_philox_advance(uint64_t* offset, hipStream_t stream);
  * the penalty P = lambda * mean_b (||G_0,b|| - center)^2 (mode 0) or lambda * mean_b
  * ||G_0,b||^2 (mode 1) into *penalty (device scalar), v = dP/dG_0, tangent and adjoint, with
  * dP/dtheta accumulated into `grads`.
+ *
+ * Threads and streams: a plan is driven by one thread at a time.  Distinct plans may be driven
+ * concurrently from several threads on distinct streams, also while one of those streams is being
+ * captured into a HIP graph: the sweeps fork their weight gradients onto a side stream that
+ * belongs to the caller's stream (one per device and caller stream, never shared between two
+ * caller streams) and join it before returning, so a capture only ever pulls its own stream's
+ * side stream into its graph.
  * ------------------------------------------------------------------------------------- */
 #define GANAMD_COP_SWAP 0
 #define GANAMD_COP_CONV 1

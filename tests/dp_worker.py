@@ -8,6 +8,10 @@ fused AdamW step, then a generator backward whose flat gradient is all-reduced t
 bench.py runs for N > 1.  Rank 0 writes the all-reduced gradients and the
 critic's parameters after its step to the path given as argv[1].
 
+``dp_worker.py OUT progan``: config 5's split (BASELINE.json: the progan pair, 4 ranks): the bench's
+progan schedule (pipeline.Iteration, fake batches one per critic step on a side stream) at
+B = 64 per rank, one iteration; rank 0 writes both models' parameters and gradients.
+
 ``dp_worker.py OUT graph``: the bench's N > 1 graph-mode path instead -- one pipelined WGAN-GP
 iteration (gan_amd.pipeline.Iteration: captured fake-batch / critic / AdamW / generator graphs,
 the next fake batch on a side stream, the flat-gradient all-reduce eagerly between graphs) at
@@ -102,8 +106,53 @@ def main_graph(out):
     dist.destroy_process_group()
 
 
+B_PROGAN = 64
+PROGAN_WORLD = 4
+
+
+def progan_seed(rank):
+    return 1960 + rank
+
+
+def make_progan(gan, dev):
+    import json
+    from oracle.params import fill_module
+    from tests._util import GOLDEN
+    with open(os.path.join(GOLDEN, "plan_progan.json")) as f:
+        pp = json.load(f)
+    G = gan.generator_3_progan.Generator(1, 256, pp["ngf"], 3)
+    D = gan.discriminator_3_wgangp_progan.Discriminator(1, pp["ndf"], 3)
+    fill_module(G, pp["g_seed"])
+    fill_module(D, pp["d_seed"])
+    return G.to(dev), D.to(dev)
+
+
+def main_progan(out):
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    import gan_amd
+    from gan_amd.pipeline import Iteration, restore, snapshot
+    dev = torch.device("cuda", 0)
+    G, D = make_progan(gan_amd, dev)
+    tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, progan_seed(rank)))
+    it = Iteration(tr, B_PROGAN, 5, world, overlap=True)       # bench.py's progan schedule (fake_schedule)
+    snap = snapshot(tr)
+    it.eager()
+    it.capture()
+    restore(tr, snap)
+    dist.barrier()
+    it.step()
+    torch.cuda.synchronize()
+    res = {k: v.detach().cpu().clone() for k, v in
+           (("g_data", tr.optimizer_G.flat.data), ("g_grad", tr.optimizer_G.flat.grad),
+            ("d_data", tr.optimizer_D.flat.data), ("d_grad", tr.optimizer_D.flat.grad))}
+    if rank == 0:
+        torch.save(dict(res, world=world), out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[2] == "graph":
-        main_graph(sys.argv[1])
-    else:
-        main(sys.argv[1])
+    mode = sys.argv[2] if len(sys.argv) > 2 else ""
+    {"graph": main_graph, "progan": main_progan}.get(mode, main)(sys.argv[1])

@@ -64,3 +64,21 @@ def test_pickled_module_checkpoint_is_refused_clearly(tmp_path):
                os.path.join(tr.ckpt_root, "old.pth"))
     with pytest.raises(RuntimeError, match="not a state_dict checkpoint"):
         tr.load_generator_ckpt("old")
+
+
+def test_checkpoint_restores_rng_streams(tmp_path):
+    """The device RNG's stream offsets travel with the checkpoint: a resumed run continues the
+    z / noise, eps and data sequences instead of redrawing the first run's numbers."""
+    _pp, tr = _trainer(tmp_path)
+    rng = tr.rng
+    data = rng.fork(2)
+    with torch.no_grad():
+        rng.offset.fill_(7)
+        data.offset.fill_((2 << rng.STREAM_SHIFT) + 11)
+    tr.save_ckpt("WGANGP", 0, 0)
+    name = os.path.splitext(os.path.basename(tr.save_ckpt("WGANGP", 0, 0)))[0]
+    _pp2, tr2 = _trainer(tmp_path)
+    assert int(tr2.rng.offset) == 0
+    assert tr2.load_generator_ckpt(name)
+    assert int(tr2.rng.offset) == 7
+    assert int(tr2.rng.fork(2).offset) == (2 << rng.STREAM_SHIFT) + 11

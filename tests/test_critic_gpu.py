@@ -426,3 +426,95 @@ def test_critic_bf16_matches_emulation(gan, B):
     assert len(errs) == 99
     assert max(errs) < 1e-6
     assert 1e-4 < gap < 2e-2        # bf16 is really on, and only at bf16's size
+
+
+def test_engine_threads_and_capture(gan):
+    """include/ganamd.h's threading contract for the critic engine (entry points
+    safe from multiple threads on distinct streams): two plans driven concurrently from two threads
+    on two streams, one of them captured into a HIP graph while the other runs eagerly.  The
+    weight-gradient side stream belongs to the caller's stream, so the capture pulls in only its
+    own; the captured replay must equal the eager run bit for bit, and every eager run of the
+    other thread must equal its single-threaded result bit for bit."""
+    import ctypes
+    import threading
+    from gan_amd import _lib, critic
+    B = 4
+    P = plan()
+
+    class Job:
+        def __init__(self, seed, xseed):
+            self.D = _make_D(gan, P["d_seed"] + seed)
+            self.x = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(xseed)).to(DEV).contiguous()
+            _zero(self.D)
+            self.run = critic.Run(critic.program_of(self.D), 1)
+            self.run._setup(self.x)
+            self.grads = self.run._grads()             # creates every .grad buffer (zeros)
+            self.gbufs = [p.grad for p in self.D.parameters() if p.grad is not None]
+            n = _lib.c_size_t(0)
+            assert _lib.LIB.ganamd_critic_workspace(self.run.plan, ctypes.byref(n)) == 0
+            self.ws = _lib.workspace(n.value, DEV)
+            self.pen = torch.zeros(1, device=DEV)
+            self.out = torch.empty(B, device=DEV)
+            self.gx = torch.empty_like(self.x)
+            self.norms = torch.empty(B, device=DEV)
+            self.stream = torch.cuda.Stream()
+
+        def step(self):                                 # on the current stream
+            for g in self.gbufs:
+                g.zero_()
+            rc = _lib.LIB.ganamd_critic_gp_step(self.run.plan, self.x.data_ptr(), 1.0, 10.0, 0, self.grads,
+                                                self.out.data_ptr(), self.gx.data_ptr(), self.norms.data_ptr(),
+                                                self.pen.data_ptr(), self.ws.data_ptr(), _lib.stream())
+            assert rc == 0
+
+        def snapshot(self):
+            return [g.clone() for g in self.gbufs] + [self.pen.clone(), self.gx.clone()]
+
+    a, b = Job(0, 91), Job(1, 92)
+    for j in (a, b):                                    # single-threaded references
+        with torch.cuda.stream(j.stream):
+            j.step()
+            j.ref = j.snapshot()
+        j.stream.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    captured = threading.Event()
+    errors, b_snaps = [], []
+
+    def capture_a():
+        try:
+            with torch.cuda.stream(a.stream):
+                with torch.cuda.graph(graph, stream=a.stream, capture_error_mode="thread_local"):
+                    a.step()
+        except Exception as e:                         # noqa: BLE001 -- reported by the main thread
+            errors.append(e)
+        finally:
+            captured.set()
+
+    def eager_b():
+        try:
+            with torch.cuda.stream(b.stream):
+                n = 0
+                while not captured.is_set() or n < 3:
+                    b.step()
+                    b_snaps.append(b.snapshot())        # device copies, checked after the join
+                    b.stream.synchronize()
+                    n += 1
+        except Exception as e:                         # noqa: BLE001
+            errors.append(e)
+
+    ta, tb = threading.Thread(target=capture_a), threading.Thread(target=eager_b)
+    tb.start()
+    ta.start()
+    ta.join(120)
+    tb.join(120)
+    assert not ta.is_alive() and not tb.is_alive(), "engine threads did not finish"
+    assert not errors, errors
+    with torch.cuda.stream(a.stream):
+        graph.replay()
+    a.stream.synchronize()
+    got = a.snapshot()
+    assert all(torch.equal(u, v) for u, v in zip(got, a.ref)), "captured replay != eager"
+    assert len(b_snaps) >= 3
+    for snap in b_snaps:
+        assert all(torch.equal(u, v) for u, v in zip(snap, b.ref)), "concurrent eager run != single-threaded"
+    print(f"engine threads: captured replay == eager; {len(b_snaps)} concurrent eager runs == single-threaded")

@@ -13,6 +13,10 @@ between captured graphs) on two ranks equals, after
 one full iteration (5 critic steps + generator step), the same iteration run here eagerly with the
 two shards one after another and their gradients averaged by hand before every optimizer step.
 
+test_dp_progan_four_ranks_match_shard_mean: config 5's split (the progan pair on 4 ranks, 64 images
+each, BASELINE.json) through the bench's progan schedule (fake batch of the next critic step on a
+side stream) against the four shards run one after another with hand-averaged gradients.
+
 test_bench_two_ranks: ``bench.py --gpus 2 --backend gloo`` starts its own ranks and reports
 n_gpus 2 (it used to run one rank silently), in eager and in graph mode.
 """
@@ -137,6 +141,76 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path):
     errs["g_move"] = float((got["g_data"] - want["g_data"].cpu()).double().norm() / (want["g_data"].cpu() - g0).double().norm())
     errs["d_move"] = float((got["d_data"] - want["d_data"].cpu()).double().norm() / (want["d_data"].cpu() - d0).double().norm())
     print("graph-mode DP vs shard mean:", errs)
+    assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
+    assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
+
+
+def _shard_mean_iteration(tr, rngs, B, groups):
+    """One WGAN-GP iteration with the shards run one after another on the same weights and the
+    gradients of every optimizer step averaged by hand (gloo: SUM, then * 1/N)."""
+    n = len(rngs)
+    for k in set(groups):
+        tr.generate_fakes(k, B)    # warm-up: the workers' warm-up recorded the noise shapes
+    fakes = []                     # each rank's fake batches, group by group (G is fixed until the G step)
+    for rng in rngs:
+        tr.rng = rng
+        fakes.append([f for k in groups for f in tr.generate_fakes(k, B)])
+
+    def mean_into(flat_grad, gs):
+        acc = gs[0].clone()
+        for g in gs[1:]:
+            acc.add_(g)
+        flat_grad.copy_(acc).mul_(1.0 / n)
+
+    for i in range(5):
+        gs = []
+        for r, rng in enumerate(rngs):
+            tr.rng = rng
+            tr.discriminator_backward(rng.fork(2).randn((B, 3, 64, 64)), B, gen_imgs=fakes[r][i])
+            gs.append(tr.optimizer_D.flat.grad.detach().clone())
+        assert _rel(gs[0].cpu(), gs[1].cpu()) > 1e-2       # the shards really differ
+        mean_into(tr.optimizer_D.flat.grad, gs)
+        tr.optimizer_D.step()
+    gs = []
+    for rng in rngs:
+        tr.rng = rng
+        tr.generator_backward(B)
+        gs.append(tr.optimizer_G.flat.grad.detach().clone())
+    mean_into(tr.optimizer_G.flat.grad, gs)
+    tr.optimizer_G.step()
+    torch.cuda.synchronize()
+
+
+def _dp_errors(got, tr, g0, d0):
+    want = {"g_data": tr.optimizer_G.flat.data, "g_grad": tr.optimizer_G.flat.grad,
+            "d_data": tr.optimizer_D.flat.data, "d_grad": tr.optimizer_D.flat.grad}
+    errs = {k: _rel(got[k], v.detach().cpu()) for k, v in want.items()}
+    errs["g_move"] = float((got["g_data"] - want["g_data"].cpu()).double().norm() / (want["g_data"].cpu() - g0).double().norm())
+    errs["d_move"] = float((got["d_data"] - want["d_data"].cpu()).double().norm() / (want["d_data"].cpu() - d0).double().norm())
+    return errs
+
+
+def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
+    out = str(tmp_path / "rank0_progan.pt")
+    W = dp_worker.PROGAN_WORLD
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={W}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
+           "progan"]
+    r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert got["world"] == W
+
+    import gan_amd
+    dev = torch.device("cuda", 0)
+    B = dp_worker.B_PROGAN
+    G, D = dp_worker.make_progan(gan_amd, dev)
+    tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, 1))
+    g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
+    rngs = [gan_amd.DeviceRNG(dev, dp_worker.progan_seed(r)) for r in range(W)]
+    _shard_mean_iteration(tr, rngs, B, [1] * 5)
+    errs = _dp_errors(got, tr, g0, d0)
+    print(f"progan {W}-rank DP vs shard mean:", errs)
     assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
     assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
 
