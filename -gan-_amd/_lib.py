@@ -42,7 +42,7 @@ class GTile(ctypes.Structure):
 
 class PackJob(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p)] + \
-               [(n, ctypes.c_int32) for n in ("sm", "sc", "st", "M", "Ck", "T", "Mpad", "Ckp", "ps", "pk", "ppad")] + \
+               [(n, ctypes.c_int32) for n in ("sm", "sc", "st", "M", "Ck", "T", "Mpad", "Ckp", "ps", "pk", "ppad", "x3")] + \
                [("chunk0", ctypes.c_int64)]
 
 

@@ -36,6 +36,7 @@
 #include <type_traits>
 
 #include "../../include/ganamd.h"
+#include "patch.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -488,10 +489,26 @@ __device__ __forceinline__ float pack_elem(const ganamd_pack_job& j, unsigned i)
   return (m < j.M && c < j.Ck) ? j.w[(unsigned)(m * j.sm + c * j.sc) + t * (unsigned)j.st] : 0.f;
 }
 
+// Element i of a packed copy: the fp32 value, and with x3 also its three bf16 planes after the
+// copy (plane p element i at ((ushort*)(out + total))[p * total + i]; x = h + m + l exactly)
+__device__ __forceinline__ void pack_store(const ganamd_pack_job& j, unsigned total, unsigned i, float v) {
+  j.out[i] = v;
+  if (j.x3) {
+    unsigned short* pl = reinterpret_cast<unsigned short*>(j.out + total);
+    const __bf16 h = (__bf16)v;
+    const float r = v - (float)h;
+    const __bf16 m = (__bf16)r;
+    const __bf16 l = (__bf16)(r - (float)m);
+    pl[i] = __builtin_bit_cast(unsigned short, h);
+    pl[total + i] = __builtin_bit_cast(unsigned short, m);
+    pl[2 * total + i] = __builtin_bit_cast(unsigned short, l);
+  }
+}
+
 __global__ void pack_a_kernel(ganamd_pack_job j) {
   const unsigned total = (unsigned)j.Mpad * j.T * j.Ckp;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
-    j.out[i] = pack_elem(j, i);
+    pack_store(j, total, i, pack_elem(j, i));
 }
 
 
@@ -1227,251 +1244,6 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
   conv_epilogue<C, MODE>(p, acc, n0, m0, split, lane, wm, wn);
 }
 
-// ---- LDS-patch conv: stride 1, "same" padding, K x K taps (K = 3, 5), maps 32 / 64 wide ----------
-// The implicit GEMM above gathers its B operand per K-step straight from global memory: every
-// input pixel is fetched once per TAP (25 times for a 5x5 conv), and its LDS tiles need a block
-// barrier per K-step; at the 3 waves per SIMD it runs at, the fp32 MFMA pipe sustains ~111-120
-// TF/s on real data (profiles/r02_mfma_ceiling_waves.txt; 154.5 at 1-2 waves).
-//
-// This kernel stages, per 16-channel chunk, the block's input PATCH with its halo --
-// P[(TH+K-1)(TW+K-1)][16], channel-minor -- in LDS once, and runs all K*K taps of the chunk on it:
-// tap (kh, kw)'s B fragment of pixel (i, j) is patch position (i + kh, j + kw), read with the
-// conflict-free [row][k] ds_read_b64 pattern of the GEMM's tiles.  The A operand (packed weights,
-// [Mpad][T][Ckp], the same few hundred KB for every block: L2/L1-resident) goes straight from
-// global memory into each wave's registers, one tap ahead -- no LDS stage and no barrier per
-// K-step: a block synchronises once per 16-channel CHUNK (25 taps of a 5x5 conv), when the
-// double-buffered patch swaps.  The next chunk's patch is fetched into registers during the
-// chunk's first tap and written to the idle buffer at its second, so those registers are free for
-// the rest of the chunk.  The modulated conv's x-scales s[c][b] (b is fixed per block) multiply
-// the A fragments in registers.
-//
-// Block: BM output channels x 512 pixels of ONE image (TH = 512 / TW rows of the full width
-// TW = W), 8 waves (wave w owns pixels 64w .. 64w + 63), one block per CU = 2 waves per SIMD.
-// Block order: row tiles of one pixel region run together (they share the patch in L2).
-constexpr int kPatchPix = 512, kPatchThreads = 512;
-
-// DGRAD: the input gradient of a stride-1 "same" conv, interior of the padded frame: a zero-padded
-// correlation of gy with the taps reversed (A is the dgrad-packed weight [Cin][T][Cout]; tap t of
-// the forward is read as tap T-1-t); replication padding adds the frame's ring afterwards
-// (ganamd_conv_dgrad).
-template <int BM, int KK, int TW, bool BSCALE, bool DGRAD>
-__global__ __launch_bounds__(kPatchThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void conv_patch_kernel(ConvArgs p) {
-  constexpr bool ZERO = DGRAD;
-  constexpr int NT = kPatchThreads;
-  constexpr int MB = (BM % 32 == 0) ? 32 : 16;          // MFMA block edge (48 rows: 16x16x4)
-  constexpr int TM = BM / MB, TN = 64 / MB, NR = MB == 32 ? 16 : 4;
-  constexpr int HS = MB == 32 ? 2 : 1;                    // half-steps (4 k per lane) per tap
-  constexpr int KPL = 4 * HS;                             // k values per lane per tap
-  using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
-  constexpr int TH = kPatchPix / TW, PAD = (KK - 1) / 2, T = KK * KK;
-  constexpr int PW = TW + KK - 1, NPOS = (TH + KK - 1) * PW;
-  constexpr int kPatchStoreTap = T > 4 ? 3 : T - 1;
-  __shared__ __attribute__((aligned(16))) float Ps[2][NPOS * LDK];
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const Gather& g = p.g;
-  const int H = g.H, W = g.W, HW = H * W;
-  const int ty = blockIdx.x % p.gy, reg = blockIdx.x / p.gy;
-  const int tiles_img = H / TH;
-  const int b = reg / tiles_img, oh0 = (reg - b * tiles_img) * TH;
-  const int m0 = ty * BM;
-  const int nct = p.Ckp / BK;
-
-  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
-  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
-  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
-  const unsigned cs4 = 4u * (unsigned)(g.B * HW);       // one channel row of the source
-
-  // The patch is fetched in units of 4 channels at one position, u = cg * NPOS + pos (pos fastest:
-  // consecutive lanes read consecutive columns; a unit's 4 loads differ by a constant channel
-  // stride, and it lands in LDS as two ds_write_b64).  Threads past the last unit redo unit
-  // NU - 1 (same values, same LDS words).  u is made opaque so its index math is redone per
-  // chunk instead of being hoisted into live registers.
-  constexpr int NU = NPOS * (BK / 4), UPT = (NU + NT - 1) / NT;
-  auto patch_load = [&](int cc, f32x4 (&pv)[UPT]) {
-#pragma unroll
-    for (int e = 0; e < UPT; ++e) {
-      int u = min(tid + e * NT, NU - 1);
-      asm volatile("" : "+v"(u));
-      const int cg = u / NPOS, pos = u - cg * NPOS;
-      const int pr = pos / PW, pc = pos - pr * PW;
-      int ih = oh0 - PAD + pr, iw = pc - PAD;
-      bool in = true;
-      if constexpr (ZERO) {
-        in = ih >= 0 && ih < H && iw >= 0 && iw < W;
-      } else {
-        ih = min(max(ih, 0), H - 1);
-        iw = min(max(iw, 0), W - 1);
-      }
-      // channels past the source's end fall outside the buffer: the hardware returns 0
-      const unsigned off = 4u * (unsigned)(b * HW + ih * W + iw) + (unsigned)(cc * BK + 4 * cg) * cs4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pv[e][q] = bload(rx, in ? (int)(off + q * cs4) : kOOB);
-    }
-  };
-  auto patch_store = [&](float* P, const f32x4 (&pv)[UPT]) {
-#pragma unroll
-    for (int e = 0; e < UPT; ++e) {
-      int u = min(tid + e * NT, NU - 1);
-      asm volatile("" : "+v"(u));
-      const int cg = u / NPOS, pos = u - cg * NPOS;
-      float* d = P + pos * LDK + 4 * cg;
-      *reinterpret_cast<f32x2*>(d) = f32x2{pv[e][0], pv[e][1]};
-      *reinterpret_cast<f32x2*>(d + 2) = f32x2{pv[e][2], pv[e][3]};
-    }
-  };
-
-  // Lane fragment maps (k of this lane within a 16-deep K-step):
-  //   32x32x2: lane (r, h) supplies k = 8h + 4hk + s in half-step hk, step s = 0..3
-  //   16x16x4: lane (r, q) supplies k = 4q + s, s = 0..3 (one half-step per tap)
-  const int fr = MB == 32 ? (lane & 31) : (lane & 15);
-  const int fk = MB == 32 ? 8 * (lane >> 5) : 4 * (lane >> 4);
-  // A fragments of one tap from global memory: rows m0 + i*MB + fr, k = fk .. fk + KPL - 1
-  int a_off[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) a_off[i] = 4 * ((m0 + i * MB + fr) * (T * p.Ckp) + fk);
-  auto a_load = [&](int kt, f32x4 (&fa)[TM][HS]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int hk = 0; hk < HS; ++hk) fa[i][hk] = bload4(rw, a_off[i] + kt * (BK * 4) + 16 * hk);
-  };
-  // x-scales of this lane's k values in chunk cc (modulated conv)
-  auto s_load = [&](int cc, f32x4 (&sv)[HS]) {
-    if constexpr (BSCALE) {
-#pragma unroll
-      for (int hk = 0; hk < HS; ++hk)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sv[hk][q] = bload(rsc, 4 * ((cc * BK + fk + 4 * hk + q) * g.B + b));
-    }
-  };
-
-  // patch position of each of this lane's B columns at tap (0, 0)
-  int posb[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int q = wv * 64 + j * MB + (lane & (MB - 1));
-    posb[j] = (q / TW) * PW + q % TW;
-  }
-
-  acc_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
-
-  auto b_read = [&](const float* __restrict__ P, int toff, int hk, float (&fb)[TN][4]) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* src = P + (posb[j] + toff) * LDK + fk + 4 * hk;
-      const f32x2 t0 = *reinterpret_cast<const f32x2*>(src), t1 = *reinterpret_cast<const f32x2*>(src + 2);
-      fb[j][0] = t0[0]; fb[j][1] = t0[1]; fb[j][2] = t1[0]; fb[j][3] = t1[1];
-    }
-  };
-  auto mfma4 = [&](const f32x4 (&fa)[TM][HS], int hk, const f32x4 (&sv)[HS], const float (&fb)[TN][4]) {
-    f32x4 a[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) a[i] = BSCALE ? fa[i][hk] * sv[hk] : fa[i][hk];
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (MB == 32)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
-          else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s4], fb[j][s4], acc[i][j], 0, 0, 0);
-        }
-  };
-
-  // prologue: chunk 0's patch, tap 0's A fragments and the chunk's scales
-  f32x4 fa[2][TM][HS], sv[HS];
-  {
-    f32x4 pv[UPT];
-    patch_load(0, pv);
-    a_load(DGRAD ? T - 1 : 0, fa[0]);
-    s_load(0, sv);
-    patch_store(Ps[0], pv);
-  }
-  __syncthreads();
-  for (int cc = 0; cc < nct; ++cc) {
-    const float* P = Ps[cc & 1];
-    const bool more_chunks = cc + 1 < nct;
-    f32x4 pv[UPT];
-    int kh = 0, kw = 0;
-#pragma unroll 1
-    for (int t = 0; t < T; t += 2) {
-      // two taps per iteration (register double buffer fa[0] / fa[1] without dynamic indexing)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tt = t + u;
-        if (tt < T) {
-          const int kt = cc * T + tt;
-          if (kt + 1 < nct * T) {                                    // next tap's weights
-            const int nt = (tt + 1 == T) ? 0 : tt + 1, nc = (tt + 1 == T) ? cc + 1 : cc;
-            a_load(nc * T + (DGRAD ? T - 1 - nt : nt), fa[u ^ 1]);
-          }
-          if (tt == 0 && more_chunks) patch_load(cc + 1, pv);      // next chunk's patch
-          const int toff = kh * PW + kw;
-          float fb[2][TN][4];
-          b_read(P, toff, 0, fb[0]);
-#pragma unroll
-          for (int hk = 0; hk < HS; ++hk) {
-            if (hk + 1 < HS) b_read(P, toff, hk + 1, fb[(hk + 1) & 1]);
-            __builtin_amdgcn_sched_barrier(0);
-            mfma4(fa[u], hk, sv, fb[hk & 1]);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          // the idle buffer (last read in chunk cc - 1); a few taps after the loads were issued
-          if (tt == kPatchStoreTap && more_chunks) patch_store(Ps[(cc + 1) & 1], pv);
-          if (++kw == KK) {
-            kw = 0;
-            ++kh;
-          }
-        }
-      }
-      if (T % 2 == 1 && t + 2 > T) {
-        // odd tap count: the last tap used fa[0] and prefetched into fa[1]; realign
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int hk = 0; hk < HS; ++hk) fa[0][i][hk] = fa[1][i][hk];
-      }
-    }
-    if (more_chunks) {
-      if (T == 1) patch_store(Ps[(cc + 1) & 1], pv);
-      s_load(cc + 1, sv);
-      __syncthreads();            // chunk cc + 1's patch is complete; chunk cc's buffer is free
-    }
-  }
-
-  // epilogue: the GEMM kernel's, with the block's pixel -> output column map
-  const int n_img = b * HW + oh0 * W;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int q = wv * 64 + j * MB + (lane & (MB - 1));
-    const int col = n_img + (q / TW) * W + q % TW;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int m = m0 + i * MB + mfma_row<MB>(lane, r);
-        if (m >= p.M) continue;
-        float v = p.alpha * acc[i][j][r];
-        if (p.oscale) v *= p.oscale[m * g.B + b];
-        if (p.bias) v += p.bias[m];
-        if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
-        if (p.act) v = v > 0.f ? v : p.act[m] * v;
-        p.y[(long)m * p.ldy + col] = v;
-      }
-    }
-  }
-}
-
 // Batched repack: block b finds its job by binary search over the jobs' chunk offsets and packs
 // kPackChunk consecutive elements of that job's GEMM-order output.
 constexpr int kPackChunk = 4096;
@@ -1499,7 +1271,8 @@ __device__ void pack_tile(const ganamd_pack_job& j, long tile, float* lds) {
   __syncthreads();
   for (int idx = threadIdx.x; idx < span * BK; idx += blockDim.x) {
     const int mr = idx / (T * BK), rem = idx - mr * T * BK, t = rem / BK, c16 = rem - t * BK;
-    j.out[(((long)(m0 + mr) * nct + cc) * T + t) * BK + c16] = lds[c16 * (R * T + 1) + mr * T + t];
+    pack_store(j, (unsigned)j.Mpad * T * j.Ckp, (unsigned)((((long)(m0 + mr) * nct + cc) * T + t) * BK + c16),
+               lds[c16 * (R * T + 1) + mr * T + t]);
   }
 }
 
@@ -1519,7 +1292,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const ganamd_pack_job* 
   const unsigned total = (unsigned)j.Mpad * j.T * j.Ckp;
   const unsigned i0 = (unsigned)(b - j.chunk0) * kPackChunk;
   const unsigned i1 = min(total, i0 + kPackChunk);
-  for (unsigned i = i0 + threadIdx.x; i < i1; i += 256) j.out[i] = pack_elem(j, i);
+  for (unsigned i = i0 + threadIdx.x; i < i1; i += 256) pack_store(j, total, i, pack_elem(j, i));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2108,12 +1881,13 @@ ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16
   return pl;
 }
 
-// bytes of the packed A operand of a conv GEMM (rows padded to the tile, K to whole K-steps)
-size_t pack_bytes(int M, int Ck, int T) {
+// bytes of the packed A operand of a conv GEMM (rows padded to the tile, K to whole K-steps); x3:
+// plus its three bf16 planes (the patch conv's operand)
+size_t pack_bytes(int M, int Ck, int T, bool x3 = false) {
   int bm, bn;
   conv_tile(M, &bm, &bn);
   const size_t mpad = (size_t)((M + bm - 1) / bm) * bm;
-  return sizeof(float) * mpad * T * (size_t)((Ck + BK - 1) / BK * BK);
+  return (x3 ? 10 : 4) * mpad * T * (size_t)((Ck + BK - 1) / BK * BK);
 }
 
 template <int BM, int BN, int WGM, int WGN, bool SCALED>
@@ -2505,105 +2279,37 @@ hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---- the split6 LDS-patch conv (conv_patch.hip) ----------------------------------------------
+// bit 0: forward, bit 1: dgrad interior through the patch conv where its domain and grid fit
+// (ganamd_conv_set_patch: A/B of the two paths; default both)
+std::atomic<int> g_patch{3};
+int patch_enabled() { return g_patch.load(std::memory_order_relaxed); }
+
+// The packed operand carries the three bf16 planes the patch conv reads (after the fp32 copy the
+// gather GEMM reads) whenever the GEMM's geometry is in the patch kernel's domain -- a function of
+// the geometry alone, so every copy of one weight has the same layout whatever math or mask is on.
+bool patch_packed(int M, int H, int W, int K, int stride, int pad, int OH, int OW) {
+  return ganamd_patch::domain(M, H, W, K, stride, pad, OH, OW);
+}
+long patch_blocks(int M, int B, int H, int W) {
+  ganamd_patch::Args a{};
+  a.M = M;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  return ganamd_patch::blocks(a);
+}
+// ... and where it runs: fp32 math, enabled, and a grid of at least one block per CU whose last
+// round is full or follows another (these long one-per-CU blocks leave a half-empty last round idle)
+bool patch_geometry(int M, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math, bool dgrad) {
+  if (!(patch_enabled() & (dgrad ? 2 : 1)) || math != GANAMD_MATH_F32 || !patch_packed(M, H, W, K, stride, pad, OH, OW))
+    return false;
+  const long blocks = patch_blocks(M, B, H, W), cus = num_cus();
+  return blocks >= cus && (blocks % cus == 0 || blocks >= 2 * cus);
+}
+
 // p.w/sm/sc/st describe the weights as stored, unless `prepacked` (then p.w is already the
 // GEMM-order operand); otherwise `packed` (pack_bytes) receives the GEMM-order copy first.
-// ---- patch-conv dispatch ----------------------------------------------------------------------
-// GANAMD_PATCH bit 0: forward, bit 1: dgrad through the LDS-patch conv.  Off by default: faster in
-// isolation (96-ch 5x5 modconv 102 -> 111 TF/s, its dgrad 95 -> 101) but slower in the iteration
-// (41.4-42.0 img/s off vs 40.3-40.9 with either or both on, profiles/r03_ab_patch_iteration.txt):
-// its one 512-thread block per CU with a 117 KB LDS patch leaves no room for the kernels of the
-// concurrent streams (ResnetInit's branches, the side-stream fake batch) that the gather GEMM's
-// smaller blocks share the CUs with.
-std::atomic<int> g_patch{-1};
-
-int patch_enabled() {
-  int v = g_patch.load(std::memory_order_relaxed);
-  if (v < 0) {
-    v = env_int("GANAMD_PATCH", 0);
-    g_patch.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-
-template <int BM, int KK, int TW, bool BSCALE, bool DGRAD>
-int patch_occ() {
-  static const int v = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_patch_kernel<BM, KK, TW, BSCALE, DGRAD>, kPatchThreads, 0) !=
-            hipSuccess || n <= 0)
-      n = 1;
-    return n;
-  }();
-  return v;
-}
-
-template <int BM, int KK, int TW, bool BSCALE, bool DGRAD>
-hipError_t launch_patch(ConvArgs p, hipStream_t st, bool dry, int* occ) {
-  if (occ) *occ = patch_occ<BM, KK, TW, BSCALE, DGRAD>();
-  if (dry) return hipSuccess;
-  p.gy = (p.M + BM - 1) / BM;
-  const long blocks = (long)p.gy * p.g.B * (p.g.H / (kPatchPix / TW));
-  hipLaunchKernelGGL((conv_patch_kernel<BM, KK, TW, BSCALE, DGRAD>), dim3((unsigned)blocks), dim3(kPatchThreads), 0, st,
-                     p);
-  return hipGetLastError();
-}
-
-template <int KK, int TW, bool BSCALE, bool DGRAD>
-hipError_t patch_bm(const ConvArgs& p, int bm, hipStream_t st, bool dry, int* occ) {
-  switch (bm) {
-    case 48:
-      if constexpr (TW == 64) return launch_patch<48, KK, TW, BSCALE, DGRAD>(p, st, dry, occ);
-      return hipErrorInvalidValue;
-    case 64: return launch_patch<64, KK, TW, BSCALE, DGRAD>(p, st, dry, occ);
-    case 96: return launch_patch<96, KK, TW, BSCALE, DGRAD>(p, st, dry, occ);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// The patch kernel's row tile: the packing tile (conv_bm, so the packed A is shared), except that
-// 128-row tiles run as two 64-row ones (128 accumulators per wave do not fit 2 waves per SIMD).
-int patch_bm_of(int M) {
-  const int bm = conv_bm(M);
-  return bm == 128 ? 64 : bm;
-}
-
-// The patch kernel's domain: stride 1, "same" padding (replicate or zero), square K = 3 / 5, the
-// full map width 32 or 64 as the tile width (TH = 256 / W rows per block), fp32, and enough blocks
-// for one full round of 2 per CU (smaller grids keep the gather GEMM with its split-K tails).
-bool patch_geometry(int M, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math, bool dgrad) {
-  if (!(patch_enabled() & (dgrad ? 2 : 1)) || math != GANAMD_MATH_F32 || stride != 1 || (K != 3 && K != 5) || pad != (K - 1) / 2 ||
-      OH != H || OW != W || (W != 32 && W != 64))
-    return false;
-  const int bm = patch_bm_of(M);
-  if (bm < 48 || (bm == 48 && W != 64)) return false;
-  const int th = kPatchPix / W;
-  if (H % th) return false;
-  // one block per CU: whole rounds, or a last round at least 90 % full (a half-empty last round
-  // of these long blocks costs more than the gather GEMM's split-K tail: B = 96 critic probe,
-  // 384 blocks on 256 CUs, 97 vs 112 TF/s)
-  const long blocks = (long)((M + bm - 1) / bm) * B * (H / th);
-  const long cus = num_cus(), rounds = (blocks + cus - 1) / cus;
-  return blocks >= cus && blocks >= 0.9 * rounds * cus;
-}
-
-template <bool DGRAD>
-hipError_t dispatch_patch_z(const ConvArgs& p, int K, int bm, hipStream_t st, bool dry, int* occ) {
-  const bool s = p.g.scale != nullptr;
-  if (p.g.W == 64) {
-    if (K == 3) return s ? patch_bm<3, 64, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<3, 64, false, DGRAD>(p, bm, st, dry, occ);
-    return s ? patch_bm<5, 64, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<5, 64, false, DGRAD>(p, bm, st, dry, occ);
-  }
-  if (K == 3) return s ? patch_bm<3, 32, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<3, 32, false, DGRAD>(p, bm, st, dry, occ);
-  return s ? patch_bm<5, 32, true, DGRAD>(p, bm, st, dry, occ) : patch_bm<5, 32, false, DGRAD>(p, bm, st, dry, occ);
-}
-
-// fwd: replication padding (every hot-path conv; zero-padded forwards keep the gather GEMM);
-// dgrad: the zero-padded, tap-reversed interior (ganamd_conv_dgrad)
-hipError_t dispatch_patch(const ConvArgs& p, int K, bool dgrad, hipStream_t st, bool dry = false, int* occ = nullptr) {
-  const int bm = patch_bm_of(p.M);
-  return dgrad ? dispatch_patch_z<true>(p, K, bm, st, dry, occ) : dispatch_patch_z<false>(p, K, bm, st, dry, occ);
-}
-
 hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab, hipStream_t st) {
   const ConvPlan pl = conv_plan(p.M, p.N, p.Ck, p.T, p.g.mode, p.g.scale != nullptr, p.bf16 != 0);
   if ((pl.slab_elems && !slab) || (!prepacked && !packed)) return hipErrorInvalidValue;
@@ -2612,7 +2318,7 @@ hipError_t dispatch_conv(ConvArgs p, bool prepacked, float* packed, float* slab,
   p.Ckp = (p.Ck + BK - 1) / BK * BK;
   if (p.ldy == 0) p.ldy = p.N;   // output rows are the GEMM rows unless a phase remap says otherwise
   if (!prepacked) {
-    launch_pack(ganamd_pack_job{p.w, packed, p.sm, p.sc, p.st, p.M, p.Ck, p.T, mpad, p.Ckp, 1, 0, 0, 0}, st);
+    launch_pack(ganamd_pack_job{p.w, packed, p.sm, p.sc, p.st, p.M, p.Ck, p.T, mpad, p.Ckp, 1, 0, 0, 0, 0}, st);
     p.w = packed;
   }
   p.w_bytes = 4 * mpad * p.T * p.Ckp;
@@ -2790,13 +2496,52 @@ static bool fwd_phased(const ganamd_conv_desc* d) {
          d->OW % d->stride == 0;
 }
 
+// Whether op's packed copy also carries the bf16 planes of the patch conv (patch_packed): the
+// replicate-padded forward and the (frame-split) dgrad of a stride-1 same conv in its domain.
+static bool pack_x3(const ganamd_conv_desc* d, int op) {
+  if (d->transposed || d->KH != d->KW) return false;
+  if (op == GANAMD_CONV_FWD)
+    return d->pad_mode == GANAMD_PAD_REPLICATE &&
+           patch_packed(d->Cout, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW);
+  return op == GANAMD_CONV_DGRAD && !dgrad_scatter(d) &&
+         patch_packed(d->Cin, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW);
+}
+
 static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed) {
   int M, Ck, T, sm, sc, bm, bn;
   a_operand(d, op, &M, &Ck, &T, &sm, &sc);
   conv_tile(M, &bm, &bn);
   const bool ph = op == GANAMD_CONV_FWD && fwd_phased(d);
   return ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, (M + bm - 1) / bm * bm, (Ck + BK - 1) / BK * BK,
-                         ph ? d->stride : 1, ph ? d->KH : 0, ph ? d->pad : 0, 0};
+                         ph ? d->stride : 1, ph ? d->KH : 0, ph ? d->pad : 0, pack_x3(d, op) ? 1 : 0, 0};
+}
+
+// the patch conv's arguments from the GEMM's (p: its A rows / K layout, gather source and epilogue)
+static ganamd_patch::Args patch_args(const ConvArgs& p, const float* packed, int mpad, int K, bool dgrad) {
+  ganamd_patch::Args a{};
+  const int wplane = mpad * p.T * p.Ckp;
+  a.w = reinterpret_cast<const unsigned short*>(packed + wplane);
+  a.wplane = wplane;
+  a.w_bytes = 6 * wplane;
+  a.M = p.M;
+  a.Ckp = p.Ckp;
+  a.KK = K;
+  a.src = p.g.src;
+  a.scale = p.g.scale;
+  a.C = p.g.C;
+  a.B = p.g.B;
+  a.H = p.g.H;
+  a.W = p.g.W;
+  a.y = p.y;
+  a.ldy = p.ldy;
+  a.bias = p.bias;
+  a.oscale = p.oscale;
+  a.noise = p.noise;
+  a.noise_scale = p.noise_scale;
+  a.act = p.act;
+  a.alpha = p.alpha;
+  a.dgrad = dgrad ? 1 : 0;
+  return a;
 }
 
 // The frame-split dgrad's ring buffer (replication padding only: zero padding drops the ring)
@@ -2824,7 +2569,7 @@ int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes) {
   if (!desc_ok(d) || !bytes || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
   int M, Ck, T, sm, sc;
   a_operand(d, op, &M, &Ck, &T, &sm, &sc);
-  *bytes = pack_bytes(M, Ck, T);
+  *bytes = pack_bytes(M, Ck, T, pack_x3(d, op));
   return GANAMD_OK;
 }
 
@@ -2842,17 +2587,21 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
   else
     dgrad_gemm(d, &M, &N, &Ck, &T);
   const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
-  if (op == GANAMD_CONV_FWD && !d->transposed && d->KH == d->KW && d->pad_mode == GANAMD_PAD_REPLICATE &&
-      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, false)) {
-    ConvArgs p{};
-    p.M = M;
-    p.g.W = d->W;
-    p.g.scale = scaled ? reinterpret_cast<const float*>(info) : nullptr;   // selects the instance only
-    p.g.mode = d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero;
-    int occ = 0;
-    (void)dispatch_patch(p, d->KH, false, nullptr, true, &occ);
-    const int bm = patch_bm_of(M), gy = (M + bm - 1) / bm, gx = d->B * (d->H / (kPatchPix / d->W));
-    const int v[11] = {bm, kPatchPix, gx, gy, gx, 1, ((Ck + BK - 1) / BK) * T, gx * gy, occ, num_cus(), 1};
+  const int Mp = op == GANAMD_CONV_FWD ? d->Cout : d->Cin;
+  if (pack_x3(d, op) && patch_geometry(Mp, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math,
+                                       op == GANAMD_CONV_DGRAD)) {
+    ganamd_patch::Args a{};
+    a.M = Mp;
+    a.B = d->B;
+    a.H = d->H;
+    a.W = d->W;
+    a.KK = d->KH;
+    a.dgrad = op == GANAMD_CONV_DGRAD;
+    a.scale = scaled ? reinterpret_cast<const float*>(info) : nullptr;   // selects the instance only
+    const int bm = ganamd_patch::row_tile(Mp), gy = (Mp + bm - 1) / bm;
+    const int blocks = (int)ganamd_patch::blocks(a), gx = blocks / gy;
+    const int v[11] = {bm, ganamd_patch::block_pixels(d->W), gx, gy, gx, 1, ((Ck + BK - 1) / BK) * T, blocks,
+                       ganamd_patch::occupancy(a), num_cus(), 1};
     for (int i = 0; i < 11; ++i) info[i] = v[i];
     return GANAMD_OK;
   }
@@ -2897,7 +2646,7 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   *bytes = 0;
   if (op == GANAMD_CONV_FWD) {
     fwd_gemm(d, &M, &N, &Ck, &T);
-    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, d->KH * d->KW))) +
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, d->KH * d->KW, pack_x3(d, op)))) +
              slab_bytes(M, N, Ck, T, fwd_mode(d), d->math == GANAMD_MATH_BF16);
   } else if (op == GANAMD_CONV_DGRAD) {
     dgrad_gemm(d, &M, &N, &Ck, &T);
@@ -2906,7 +2655,7 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
     const int Nring = d->B * (Hp * Wp - d->H * d->W);
     const size_t slabs = std::max(slab_bytes(M, N, Ck, T, dgrad_mode(d), d->math == GANAMD_MATH_BF16),
                                   Nring > 0 ? slab_bytes(M, Nring, Ck, T, kTransposed, d->math == GANAMD_MATH_BF16) : 0);
-    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))) + align256(dgrad_pad_bytes(d)) +
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T, pack_x3(d, op)))) + align256(dgrad_pad_bytes(d)) +
              align256(dgrad_scatter_bytes(d)) + slabs;
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;
@@ -2964,7 +2713,7 @@ int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float*
   p.w = w;
   if (!d->packed_w) {
     float* packed = static_cast<float*>(workspace);
-    launch_pack(ganamd_pack_job{w, packed, p.sm, p.sc, p.st, p.M, p.Ck, 1, mpad, p.Ckp, 1, 0, 0, 0}, stream);
+    launch_pack(ganamd_pack_job{w, packed, p.sm, p.sc, p.st, p.M, p.Ck, 1, mpad, p.Ckp, 1, 0, 0, 0, 0}, stream);
     p.w = packed;
   }
   p.w_bytes = 4 * mpad * p.Ckp;
@@ -3008,19 +2757,19 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   p.ldy = N;
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
-  float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T))));
-  if (!d->transposed && p.g.mode == kReplicate &&
-      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, false) && d->KH == d->KW) {
-    // LDS-patch conv (conv_patch_kernel): same packed A layout as the GEMM ([Mpad][T][Ckp])
+  float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T, pack_x3(d, GANAMD_CONV_FWD)))));
+  if (pack_x3(d, GANAMD_CONV_FWD) &&
+      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, false)) {
+    // the split6 LDS-patch conv (conv_patch.hip) on the planes of the packed operand
     const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
     p.Ckp = (Ck + BK - 1) / BK * BK;
-    p.ldy = N;
+    const float* pw = w;
     if (!d->packed_w) {
-      launch_pack(ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, mpad, p.Ckp, 1, 0, 0, 0}, stream);
-      p.w = packed;
+      launch_pack(pack_job(d, GANAMD_CONV_FWD, w, packed), stream);
+      pw = packed;
     }
-    p.w_bytes = 4 * mpad * T * p.Ckp;
-    return dispatch_patch(p, d->KH, false, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+    return ganamd_patch::launch(patch_args(p, pw, mpad, d->KH, false), stream) == hipSuccess ? GANAMD_OK
+                                                                                              : GANAMD_ELAUNCH;
   }
   if (!fwd_phased(d))
     return dispatch_conv(p, d->packed_w != 0, packed, slab, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
@@ -3076,7 +2825,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   const size_t pad_bytes = dgrad_pad_bytes(d);
   char* ws = static_cast<char*>(workspace);
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
-  if (!d->packed_w) ws += align256(pack_bytes(M, Ck, T));
+  if (!d->packed_w) ws += align256(pack_bytes(M, Ck, T, pack_x3(d, GANAMD_CONV_DGRAD)));
   float* slab = reinterpret_cast<float*>(ws + align256(pad_bytes) + align256(dgrad_scatter_bytes(d)));
   const bool pre = d->packed_w != 0;
   if (dgrad_scatter(d)) {
@@ -3106,13 +2855,14 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   // frame in the epilogue (OutMap s = -1): interior -> gx, ring -> ring buffer (replication) or
   // dropped (zero padding); ring_fold_kernel then adds the ring onto the edge pixels.
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
-  if (d->KH == d->KW && patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, true)) {
-    // the frame's interior with the LDS-patch conv (zero-padded, taps reversed), then -- for
+  if (pack_x3(d, GANAMD_CONV_DGRAD) &&
+      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, true)) {
+    // the frame's interior with the split6 patch conv (zero-padded, taps reversed), then -- for
     // replication padding -- the ring alone through the gather GEMM (OutMap s = -2) and its fold
     const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
     p.Ckp = (Ck + BK - 1) / BK * BK;
     if (!pre) {
-      launch_pack(ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, mpad, p.Ckp, 1, 0, 0, 0}, stream);
+      launch_pack(pack_job(d, GANAMD_CONV_DGRAD, w, packed), stream);
       p.w = packed;
     }
     p.w_bytes = 4 * mpad * T * p.Ckp;
@@ -3121,7 +2871,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     p.N = d->B * d->H * d->W;
     p.ohw = d->H * d->W;
     p.ldy = p.N;
-    if (dispatch_patch(p, d->KH, true, stream) != hipSuccess) return GANAMD_ELAUNCH;
+    if (ganamd_patch::launch(patch_args(p, p.w, mpad, d->KH, true), stream) != hipSuccess) return GANAMD_ELAUNCH;
     if (!pad_bytes) return GANAMD_OK;
     float* ring = reinterpret_cast<float*>(ws);
     const int Rn = Hp * Wp - d->H * d->W;

@@ -1,0 +1,376 @@
+// LDS-patch convolution on the split6 pipe: stride 1, "same" padding, K x K taps (K = 3, 5),
+// maps 32 / 64 wide -- the generator's modulated convs at 32x32 / 64x64 (48- and 96-channel,
+// generator_13_5.py:219-248 in the batch-shared form) and their input gradients.
+//
+// Why not the gather GEMM (conv_gemm.hip conv_body_x3) for these: the implicit GEMM gathers its B
+// operand per K-step, so every input element is fetched, scaled by its modulation s[c][b], split
+// into three bf16 planes (h, m, l) and written to LDS once per TAP -- 25 times for a 5x5 conv.  At
+// 48 output channels that staging work per MFMA exceeds what the VALU can hide behind the matrix
+// cores (each element feeds only 48 rows), and the halo is re-fetched from L2/HBM per tap (PMC:
+// 2.06x the algorithmic bytes on the 96-channel 5x5).  Here a block stages its input PATCH -- the
+// (TH + K - 1) x (W + K - 1) positions around its TH output rows, 16 channels, already scaled and
+// split into the three planes -- once per 16-channel chunk, and runs all K*K taps on it: tap
+// (kh, kw)'s B fragment of pixel (i, j) is patch position (i + kh, j + kw).  Staging work and halo
+// traffic drop K*K-fold; what is left per tap is the MFMA work and LDS fragment reads.
+//
+// A operand: the packed weights pre-split into three bf16 planes by the pack kernels (the optimizer
+// refreshes them with the fp32 copy, conv_gemm.hip pack_x3), read straight from global memory into
+// each wave's registers one tap ahead (the same few hundred KB for every block: L1/L2 resident).
+// No LDS stage and no barrier per tap: a block synchronises once per chunk, when its double-
+// buffered patch swaps; the next chunk's patch is fetched into registers during the first tap and
+// written to the idle buffer a few taps later.
+//
+// fp32 products on the bf16 matrix cores (split6, as conv_gemm.hip): x = h + m + l exactly, the six
+// products with a high part per 16 k -- 32x32 blocks: six v_mfma_f32_32x32x16_bf16; 16-row blocks
+// (48 rows): three full-rate v_mfma_f32_16x16x32_bf16 on pairs of products.
+//
+// Block: NW waves, NPIX pixels (whole rows) of ONE image, all BM (<= 96) output channels of a row
+// tile; wave w owns pixels [w * NPIX / NW, (w + 1) * NPIX / NW).  W = 64: 512 pixels, 8 waves;
+// W = 32: 256 pixels, 4 waves.  LDS: 2 x 3 planes x positions x 16 channels x 2 B (W = 64, K = 5:
+// 153 KiB) -- one block per CU.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "patch.h"
+
+namespace ganamd_patch {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kOOB = (int)0x80000000;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+// buffer loads: an out-of-range offset returns 0 in hardware (padding / tails are a select of the
+// offset, never a branch around the load)
+__device__ __forceinline__ float bload(rsrc_t r, int off) {
+  asm("" : "+v"(off));
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ bf16x8 bload8h(rsrc_t r, int off) {   // 8 bf16 (16 bytes)
+  asm("" : "+v"(off));
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// exact 3-way split x = h + m + l (RNE; both differences are exact in fp32)
+__device__ __forceinline__ void split4(const f32x4& x, bf16x4& h, bf16x4& m, bf16x4& l) {
+  float r[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (__bf16)x[e];
+    r[e] = x[e] - (float)h[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    m[e] = (__bf16)r[e];
+    r[e] -= (float)m[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) l[e] = (__bf16)r[e];
+}
+
+// element offset of 8-channel half `half` of patch position `pos` in one plane: 32-byte rows, the
+// two 16-byte halves swapped on odd 8-position groups (conflict-free ds_read_b128 fragment reads
+// of 16 consecutive positions at any start)
+__device__ __forceinline__ int poff(int pos, int half) { return pos * 16 + 8 * (half ^ ((pos >> 3) & 1)); }
+
+template <int MB>
+__device__ __forceinline__ int mfma_row(int lane, int r) {
+  return MB == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : 4 * (lane >> 4) + r;
+}
+
+template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
+__global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
+  constexpr int NT = 64 * NW;
+  constexpr int PW = NPIX / NW;                             // pixels per wave
+  constexpr int MB = (BM % 32 == 0) ? 32 : 16;              // MFMA block edge (48 rows: 16)
+  constexpr int TM = BM / MB, TN = PW / MB, NR = MB == 32 ? 16 : 4;
+  using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
+  constexpr int TH = NPIX / TW, PAD = (KK - 1) / 2, T = KK * KK;
+  constexpr int PWD = TW + KK - 1, NPOS = (TH + KK - 1) * PWD;
+  constexpr int PS = NPOS * 16;                             // plane stride (bf16 elements)
+  constexpr int BUF = 3 * PS;
+  constexpr int NU = NPOS * 4, UPT = (NU + NT - 1) / NT;    // staging units: 4 channels at one position
+  constexpr int kStoreTap = T > 4 ? 3 : T - 1;
+  static_assert(TN >= 1 && TM * MB == BM && TN * MB == PW, "tile");
+  __shared__ __attribute__((aligned(16))) unsigned short Ps[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int H = p.H, HW = H * TW;
+  const int gy = (p.M + BM - 1) / BM;
+  const int ty = blockIdx.x % gy, reg = blockIdx.x / gy;
+  const int tiles_img = H / TH;
+  const int b = reg / tiles_img, oh0 = (reg - b * tiles_img) * TH;
+  const int m0 = ty * BM;
+  const int nct = p.Ckp / 16;
+
+  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
+  const rsrc_t rx = make_rsrc(p.src, 4 * p.C * p.B * HW);
+  const rsrc_t rsc = make_rsrc(BSCALE ? p.scale : p.src, BSCALE ? 4 * p.C * p.B : 0);
+  const unsigned cs4 = 4u * (unsigned)(p.B * HW);           // one channel row of the source
+
+  // ---- patch staging: unit u = (channel group cg of 4, position pos), pos fastest (consecutive
+  // lanes read consecutive columns).  u is opaque so its index math is redone per chunk.
+  auto patch_load = [&](int cc, f32x4 (&pv)[UPT]) {
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) {
+      int u = min(tid + e * NT, NU - 1);
+      asm volatile("" : "+v"(u));
+      const int cg = u / NPOS, pos = u - cg * NPOS;
+      const int pr = pos / PWD, pc = pos - pr * PWD;
+      int ih = oh0 - PAD + pr, iw = pc - PAD;
+      bool in = true;
+      if constexpr (DGRAD) {
+        in = ih >= 0 && ih < H && iw >= 0 && iw < TW;
+      } else {
+        ih = min(max(ih, 0), H - 1);
+        iw = min(max(iw, 0), TW - 1);
+      }
+      // channels past the source's end fall outside the buffer: the hardware returns 0
+      const unsigned off = 4u * (unsigned)(b * HW + ih * TW + iw) + (unsigned)(cc * 16 + 4 * cg) * cs4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pv[e][q] = bload(rx, in ? (int)(off + q * cs4) : kOOB);
+    }
+  };
+  auto patch_store = [&](unsigned short* P, int cc, const f32x4 (&pv)[UPT]) {
+#pragma unroll
+    for (int e = 0; e < UPT; ++e) {
+      int u = min(tid + e * NT, NU - 1);
+      asm volatile("" : "+v"(u));
+      const int cg = u / NPOS, pos = u - cg * NPOS;
+      f32x4 v = pv[e];
+      if constexpr (BSCALE) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] *= bload(rsc, 4 * ((cc * 16 + 4 * cg + q) * p.B + b));
+      }
+      bf16x4 h, m, l;
+      split4(v, h, m, l);
+      const int o = poff(pos, cg >> 1) + 4 * (cg & 1);
+      *reinterpret_cast<bf16x4*>(&P[o]) = h;
+      *reinterpret_cast<bf16x4*>(&P[PS + o]) = m;
+      *reinterpret_cast<bf16x4*>(&P[2 * PS + o]) = l;
+    }
+  };
+
+  // ---- A fragments of one tap from global memory (pre-split planes).  32x32: lane (r, h) holds
+  // rows m0 + 32i + r, k = 8h .. 8h+7 of the three planes.  16x16 paired: lane (r, q), k-half
+  // hf = q & 1, pair hi = q >> 1: (h|m), (h|l), (m|h) (see mfma below).
+  const int fr = MB == 32 ? (lane & 31) : (lane & 15);
+  const int fhalf = MB == 32 ? (lane >> 5) : ((lane >> 4) & 1);
+  const int fhi = MB == 32 ? 0 : (lane >> 5);
+  int a_row[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) a_row[i] = 2 * (((m0 + i * MB + fr) * nct * T) * 16 + 8 * fhalf);   // bytes
+  const int pl0 = MB == 32 ? 0 : (fhi ? 1 : 0), pl1 = MB == 32 ? 1 : (fhi ? 2 : 0), pl2 = MB == 32 ? 2 : (fhi ? 0 : 1);
+  const int wpb = 2 * p.wplane;                             // plane stride in bytes
+  auto a_load = [&](int kt, bf16x8 (&fa)[TM][3]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int o = a_row[i] + kt * 32;
+      fa[i][0] = bload8h(rw, o + pl0 * wpb);
+      fa[i][1] = bload8h(rw, o + pl1 * wpb);
+      fa[i][2] = bload8h(rw, o + pl2 * wpb);
+    }
+  };
+
+  // patch position of each of this lane's B columns at tap (0, 0)
+  int posb[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int q = wv * PW + j * MB + fr;
+    posb[j] = (q / TW) * PWD + q % TW;
+  }
+  const int bq0 = 0, bq1 = MB == 32 ? 1 : (fhi ? 0 : 1), bq2 = MB == 32 ? 2 : (fhi ? 2 : 1);
+  auto b_read = [&](const unsigned short* P, int toff, bf16x8 (&fb)[TN][3]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = poff(posb[j] + toff, fhalf);
+      fb[j][0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
+      fb[j][1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
+      fb[j][2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
+    }
+  };
+
+  acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
+
+  auto mfma = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TN][3]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (MB == 32) {
+          // l*h, h*l, m*m, m*h, h*m, h*h: smallest first into the same accumulator
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+        } else {
+          // (h|m)x(h|h) = hh + mh, (h|l)x(m|h) = hm + lh, (m|h)x(m|l) = mm + hl: lanes q < 2 carry
+          // the first 16-k half of the 32, q >= 2 the second (the same 16 channels)
+#pragma unroll
+          for (int t = 0; t < 3; ++t)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
+        }
+      }
+  };
+
+  // prologue: chunk 0's patch and tap 0's A fragments
+  bf16x8 fa[2][TM][3];
+  {
+    f32x4 pv[UPT];
+    patch_load(0, pv);
+    a_load(DGRAD ? T - 1 : 0, fa[0]);
+    patch_store(Ps, 0, pv);
+  }
+  __syncthreads();
+  for (int cc = 0; cc < nct; ++cc) {
+    const unsigned short* P = Ps + (cc & 1) * BUF;
+    const bool more = cc + 1 < nct;
+    f32x4 pv[UPT];
+    int kh = 0, kw = 0;
+#pragma unroll 1
+    for (int t = 0; t < T; t += 2) {
+      // two taps per iteration: register double buffer fa[0] / fa[1] without dynamic indexing
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int tt = t + u;
+        if (tt < T) {
+          const int kt = cc * T + tt;
+          if (kt + 1 < nct * T) {                               // the next tap's weights
+            const int nt = (tt + 1 == T) ? 0 : tt + 1, nc = (tt + 1 == T) ? cc + 1 : cc;
+            a_load(nc * T + (DGRAD ? T - 1 - nt : nt), fa[u ^ 1]);
+          }
+          if (tt == 0 && more) patch_load(cc + 1, pv);          // the next chunk's patch
+          bf16x8 fb[TN][3];
+          b_read(P, kh * PWD + kw, fb);
+          mfma(fa[u], fb);
+          // the idle buffer (last read in chunk cc - 1), a few taps after its loads were issued
+          if (tt == kStoreTap && more) patch_store(Ps + ((cc + 1) & 1) * BUF, cc + 1, pv);
+          if (++kw == KK) {
+            kw = 0;
+            ++kh;
+          }
+        }
+      }
+      if (T % 2 == 1 && t + 2 > T) {
+        // odd tap count: the last tap used fa[0] and prefetched into fa[1]; realign
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) fa[0][i][q] = fa[1][i][q];
+      }
+    }
+    if (more) __syncthreads();       // chunk cc + 1's patch is complete; chunk cc's buffer is free
+  }
+
+  // epilogue
+  const long n_img = (long)b * HW + (long)oh0 * TW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int q = wv * PW + j * MB + (lane & (MB - 1));
+    const long col = n_img + (q / TW) * TW + q % TW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int m = m0 + i * MB + mfma_row<MB>(lane, r);
+        if (m >= p.M) continue;
+        float v = p.alpha * acc[i][j][r];
+        if (p.oscale) v *= p.oscale[m * p.B + b];
+        if (p.bias) v += p.bias[m];
+        if (p.noise) v += p.noise_scale[m] * p.noise[(long)m * p.ldy + col];
+        if (p.act) v = v > 0.f ? v : p.act[m] * v;
+        p.y[(long)m * p.ldy + col] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
+int occ_of() {
+  static const int v = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_patch_x3_kernel<BM, NW, NPIX, KK, TW, BSCALE, DGRAD>,
+                                                     64 * NW, 0) != hipSuccess || n <= 0)
+      n = 1;
+    return n;
+  }();
+  return v;
+}
+
+// instance selection: W = 64 -> 512 pixels / 8 waves, W = 32 -> 256 pixels / 4 waves
+template <int BM, int KK, bool BSCALE, bool DGRAD>
+hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
+  if (a.W == 64) {
+    if (occ) *occ = occ_of<BM, 8, 512, KK, 64, BSCALE, DGRAD>();
+    if (!dry)
+      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, 8, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)), dim3(512),
+                         0, st, a);
+  } else {
+    if (occ) *occ = occ_of<BM, 4, 256, KK, 32, BSCALE, DGRAD>();
+    if (!dry)
+      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, 4, 256, KK, 32, BSCALE, DGRAD>), dim3((unsigned)blocks(a)), dim3(256),
+                         0, st, a);
+  }
+  return dry ? hipSuccess : hipGetLastError();
+}
+
+template <int BM, int KK>
+hipError_t go_k(const Args& a, hipStream_t st, bool dry, int* occ) {
+  const bool s = a.scale != nullptr;
+  if (a.dgrad) return s ? go<BM, KK, true, true>(a, st, dry, occ) : go<BM, KK, false, true>(a, st, dry, occ);
+  return s ? go<BM, KK, true, false>(a, st, dry, occ) : go<BM, KK, false, false>(a, st, dry, occ);
+}
+
+hipError_t dispatch(const Args& a, hipStream_t st, bool dry, int* occ) {
+  const int bm = row_tile(a.M);
+  if (bm == 48) return a.KK == 3 ? go_k<48, 3>(a, st, dry, occ) : go_k<48, 5>(a, st, dry, occ);
+  if (bm == 96) return a.KK == 3 ? go_k<96, 3>(a, st, dry, occ) : go_k<96, 5>(a, st, dry, occ);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int row_tile(int M) { return M <= 0 ? 0 : M <= 48 ? 48 : M <= 96 ? 96 : 0; }
+
+int block_pixels(int W) { return W == 64 ? 512 : W == 32 ? 256 : 0; }
+
+bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW) {
+  if (stride != 1 || (K != 3 && K != 5) || pad != (K - 1) / 2 || OH != H || OW != W || (W != 32 && W != 64))
+    return false;
+  return row_tile(M) != 0 && H % (block_pixels(W) / W) == 0;
+}
+
+long blocks(const Args& a) {
+  const int bm = row_tile(a.M), th = block_pixels(a.W) / a.W;
+  return (long)((a.M + bm - 1) / bm) * a.B * (a.H / th);
+}
+
+int occupancy(const Args& a) {
+  int occ = 1;
+  (void)dispatch(a, nullptr, true, &occ);
+  return occ;
+}
+
+hipError_t launch(const Args& a, hipStream_t st) {
+  if (!domain(a.M, a.H, a.W, a.KK, 1, (a.KK - 1) / 2, a.H, a.W) || !a.w || !a.src || !a.y) return hipErrorInvalidValue;
+  return dispatch(a, st, false, nullptr);
+}
+
+}  // namespace ganamd_patch

@@ -93,8 +93,8 @@ PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks",
 
 @contextlib.contextmanager
 def patch_conv(mask: int = 3):
-    """Route stride-1 convs through the LDS-patch direct kernel (bit 0 forward, bit 1 dgrad)
-    inside the block (ganamd_conv_set_patch; default off, see conv_gemm.hip patch_enabled)."""
+    """Which stride-1 convs take the split6 LDS-patch kernel inside the block (bit 0 forward, bit 1
+    dgrad; ganamd_conv_set_patch, default 3 = both): mask 0 runs the gather GEMM instead (A/B, tests)."""
     prev = LIB.ganamd_conv_set_patch(int(mask))
     try:
         yield

@@ -68,6 +68,9 @@ def parse():
                     help="make the next fake-batch group on a second stream during the current group's critic "
                          "steps (default: the headline schedule's FAKE_OVERLAP; groups of 1 without overlap = "
                          "one graph per phase, the reference's order)")
+    ap.add_argument("--patch", choices=["on", "off"], default="on",
+                    help="stride-1 convs on 32/64-wide maps through the split6 LDS-patch conv (default) or the "
+                         "gather GEMM (ganamd_conv_set_patch; A/B)")
     ap.add_argument("--fake-groups", default=None, metavar="K,K,...",
                     help="fake-batch groups of the n_critic steps, each one generator forward with segmented "
                          "BatchNorm (default: the headline schedule FAKE_GROUPS)")
@@ -212,8 +215,8 @@ def probe_kernel(dev, spec, reps=20):
     w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
     xs = torch.rand(g.Cin, g.B, device=dev) if spec["scaled"] else None
     ys = torch.rand(g.Cout, g.B, device=dev) if spec["scaled"] else None
-    if pl["kernel"] == 1:                                      # the LDS-patch conv (conv_gemm.hip)
-        kernel = f"conv_patch_kernel<{pl['bm']},{g.K},{g.W},{'true' if spec['scaled'] else 'false'}>"
+    if pl["kernel"] == 1:                                      # the split6 LDS-patch conv (conv_patch.hip)
+        kernel = f"conv_patch_x3_kernel<{pl['bm']},...,{g.K},{g.W},{'true' if spec['scaled'] else 'false'},false>"
     else:
         kernel = f"conv_gemm_kernel<{pl['bm']},{pl['bn']},...,{'true' if spec['scaled'] else 'false'},false>"
     y = torch.empty(g.Cout, g.B, g.OH, g.OW, device=dev)
@@ -415,6 +418,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     from gan_amd import ops
     from gan_amd.dist import allreduce_mean_
+    ops.LIB.ganamd_conv_set_patch(3 if args.patch == "on" else 0)
 
     G, D, tr, it = build(args, dev, rank, world)
     B = args.batch
@@ -564,7 +568,7 @@ def main():
             "dtype": "fp32" if args.precision == "fp32" else "bf16 GEMM operands, fp32 accumulate/storage; fp32 R1/R2/GP steps",
             "data": "synthetic N(0,1) real batches drawn on device each critic step; random reference-init weights",
             "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
-                       "parallelism": f"dp{world}", "mode": args.mode},
+                       "parallelism": f"dp{world}", "mode": args.mode, "patch_conv": args.patch},
         }
         if headline:
             out["config"]["n_critic"] = N_CRITIC

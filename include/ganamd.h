@@ -65,12 +65,15 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
 /* The block schedule conv_fwd / conv_dgrad will launch (introspection for tests and tools):
  * info[11] = {BM, BN, column tiles, row tiles, whole-tile columns, tail K-splits, K-steps per
  * split, blocks launched, resident blocks per CU of the instance, CUs, kernel (0: the gather
- * GEMM, 1: the LDS-patch conv -- BN is then its 256-pixel region)}.  scaled: whether the
- * x_scale / gy_scale operand will be passed (it selects the kernel instance). */
+ * GEMM, 1: the split6 LDS-patch conv -- BN is then its pixel region: 512 pixels at W = 64,
+ * 256 at W = 32)}.  scaled: whether the x_scale / gy_scale operand will be passed (it selects
+ * the kernel instance). */
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info);
-/* Which stride-1 convolutions take the LDS-patch direct kernel: bit 0 forward, bit 1 dgrad
- * (initially $GANAMD_PATCH, default 0).  mask < 0 only queries.  Returns the previous mask.
- * Plans are chosen at launch (or graph capture) time. */
+/* Which stride-1 "same" convolutions on 32- / 64-wide maps take the split6 LDS-patch kernel
+ * (csrc/conv_patch.hip) where its domain and grid fit: bit 0 forward, bit 1 dgrad interior
+ * (default 3 = both; 0 = the gather GEMM everywhere, for A/B).  mask < 0 only queries.  Returns
+ * the previous mask.  Plans are chosen at launch (or graph capture) time; the packed-weight
+ * layout does not depend on the mask. */
 int ganamd_conv_set_patch(int mask);
 
 /* The weight operand of conv_fwd / conv_dgrad in GEMM order (rows padded to the tile grid,
@@ -91,6 +94,8 @@ typedef struct ganamd_pack_job {
   int32_t sm, sc, st, M, Ck, T, Mpad, Ckp;
   int32_t ps, pk, ppad;   /* ps > 1: the s*s output phases of a stride-ps transposed conv (kernel pk,
                              padding ppad), each packed over its (pk/ps)^2 taps; T counts all pk^2 */
+  int32_t x3;             /* also the three bf16 planes (h, m, l: x = h + m + l exactly) of the copy,
+                             after it, for the split6 LDS-patch conv (ganamd_conv_pack_bytes counts them) */
   int64_t chunk0;
 } ganamd_pack_job;
 int ganamd_conv_pack_job(const ganamd_conv_desc* d, int op, const float* w, float* packed, ganamd_pack_job* job);

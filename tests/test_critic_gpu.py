@@ -383,9 +383,10 @@ def test_program_regularised_step_matches_autograd(gan):
     assert v1 <= 2 * v2 + 1e-4 and m1 <= 2 * m2 + 1e-4, (v1, m1, v2, m2)
 
 
-@pytest.mark.parametrize("B", [8, 64])
+@pytest.mark.parametrize("B", [8, 64, 256])
 def test_critic_bf16_matches_emulation(gan, B):
-    """Config 4's bf16 GEMMs, pinned op by op inside the network: the critic program runs with
+    """Config 4's bf16 GEMMs, pinned op by op inside the network (B = 256: the 2B samples of config
+    4's plain critic step at B = 128): the critic program runs with
     GANAMD_MATH_BF16, and every one of its 99 conv / linear outputs is re-evaluated in float64 from
     the kernel's own saved input with both GEMM operands rounded to bf16 (RNE) -- the rounding
     points of the kernels (oracle.model.BF16_GEMM does the same for whole-network runs).

@@ -211,3 +211,77 @@ def test_progan_steps_b64_vs_oracle(gan):
     print("progan generator B=64", float(g_loss.detach()), oloss, grad_norm_stats(grows, gwant), "oracle spread", spread)
     assert rel_err([float(g_loss.detach())], [oloss]) < 1e-4
     check_grads(grows, gwant, bar)
+
+
+def test_lazy_bf16_b128(gan, P):
+    """Config 4 as benchmarked: the bf16 plain critic step and the bf16 generator step at B=128
+    (train/wganlazygpR2.py:48-77, 17-27).
+
+    (1) Per op: a sample of the generator step's conv GEMM launches (forward with the x*s gather and
+        *d / noise epilogue, dgrad, wgrad; every 11th) re-evaluated in float64 with both operands
+        rounded to bf16 at the kernels' rounding points (tests/_emu.py) -- only fp32 accumulation
+        order remains, bar 1e-5.  (The critic's launches at 2B = 256: test_critic_bf16_matches_emulation.)
+    (2) End to end, the generator step against the same step in fp32 on the same inputs (device
+        Philox draws, same seed), and the plain critic step against the fp32 CPU oracle: bf16 is
+        measurably on and within bf16's reach.  Bars: losses 2e-2 (the fake loss and the
+        generator loss carry G13_5's ~100 sequential layers: 8e-2, as at B=4 in
+        test_models_gpu.py::test_lazy_bf16_steps); gradient-norm statistics median 2e-2, vector 5e-2
+        (bf16 operands carry 2^-9 relative rounding per operand; measured values are printed)."""
+    from oracle import model as om
+    from tests._emu import Recorder
+    B, seed = 128, 811
+
+    def gen_step(precision, record=False):
+        G, D = _pair(gan, P)
+        tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.DeviceRNG(DEV, seed),
+                                    precision=precision)
+        rec = Recorder(every=11, cap=40) if record else None
+        if rec:
+            with rec:
+                _gen, g_loss = tr.generator_backward(B)
+        else:
+            _gen, g_loss = tr.generator_backward(B)
+        torch.cuda.synchronize()
+        rows = _rows(G, [n for n, _, _ in P["g_params"]])
+        return float(g_loss.detach()), rows, rec
+
+    loss_bf, rows_bf, rec = gen_step("bf16", record=True)
+    assert all(c["math"] == gan._lib.MATH_BF16 for c in rec.calls) and len(rec.calls) >= 30
+    _threads()
+    rec.check(bf16=True, bars={"fwd": 1e-5, "dgrad": 1e-5, "wgrad": 1e-5})
+    del rec
+    _free()
+    loss_32, rows_32, _ = gen_step("fp32")
+    e_loss = rel_err([loss_bf], [loss_32])
+    g_stats = grad_norm_stats(rows_bf, rows_32)
+    print(f"bf16 generator step B={B}: loss {loss_bf} vs fp32 {loss_32} (rel {e_loss:.2e}); grad stats vs fp32 {g_stats}")
+    assert 1e-7 < e_loss < 8e-2
+    assert g_stats[0] < 2e-2 and g_stats[3] < 5e-2, g_stats
+    _free()
+
+    # plain critic step (idx 1: no R1/R2/GP) in bf16 vs the fp32 CPU oracle
+    img_seed, dseed = 812, 813
+    images = torch.randn(B, 3, 64, 64, generator=torch.Generator().manual_seed(img_seed))
+    G, D = _pair(gan, P)
+    tr = gan.wganlazygpR2.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(dseed, DEV),
+                                precision="bf16")
+    tr.optimizer_D.zero_grad()
+    out = tr.discriminator_backward(images.to(DEV), B, 1)
+    losses = [float(v.detach().reshape(-1)[0]) for v in out[:2]]
+    names = [n for n, _, _ in P["d_params"]]
+    rows = _rows(D, names)
+    _free(G, D, tr, out)
+    GP = om.params_from_plan(P["g_params"], P["g_seed"])
+    DP = om.params_from_plan(P["d_params"], P["d_seed"])
+    want_l = [float(v.detach().reshape(-1)[0]) for v in
+              om.WGANLazyR2(GP, DP).discriminator_trainstep(images, B, 1, om.Draw(dseed))[:2]]
+    want = np.asarray([tensor_summary(DP.t[n].grad) if n in DP.t and DP.t[n].grad is not None else [np.nan] * 11
+                       for n in names])
+    del GP, DP
+    gc.collect()
+    er, ef = rel_err(losses[:1], want_l[:1]), rel_err(losses[1:], want_l[1:])
+    d_stats = grad_norm_stats(rows, want)
+    print(f"bf16 plain critic step B={B}: losses {losses} vs fp32 oracle {want_l} (rel {er:.2e} / {ef:.2e}); "
+          f"grad stats {d_stats}")
+    assert 1e-7 < er < 2e-2 and 1e-7 < ef < 8e-2
+    assert d_stats[0] < 2e-2 and d_stats[3] < 5e-2, d_stats

@@ -504,27 +504,22 @@ def test_conv_fwd_ex_noise_act(ops):
 
 
 PATCH_CASES = [
-    # B, Cin, H, Cout, k, pad mode, scaled, noise+act: shapes the LDS-patch conv takes
-    # (conv_patch_kernel: stride 1, "same" padding, 32/64-wide maps, >= 1 round of 1 block per CU)
-    (32, 96, 64, 96, 5, 1, True, True),      # G13_5 modulated 5x5 (96 rows: 32x32x2 blocks)
-    (32, 48, 64, 48, 3, 1, True, False),     # 48 rows: 16x16x4 blocks
+    # B, Cin, H, Cout, k, pad mode, scaled, noise+act: shapes the split6 LDS-patch conv takes
+    # (conv_patch.hip: stride 1, "same" padding, 32/64-wide maps, rows M <= 48 or 72 < M <= 96,
+    # >= one full round of one block per CU)
+    (32, 96, 64, 96, 5, 1, True, True),      # G13_5 modulated 5x5 (96 rows: 32x32x16 blocks)
+    (32, 48, 64, 48, 3, 1, True, False),     # 48 rows: paired 16x16x32 blocks
     (32, 40, 64, 45, 5, 1, False, False),    # ragged rows, channels not a multiple of 16
-    (128, 128, 32, 128, 3, 1, False, False), # D9_4 block conv on the critic's 2B batch (two 64-row tiles)
-    (16, 108, 64, 108, 5, 1, False, True),   # the ToRGB pre-conv rows (128-row packing, 64-row tiles)
-    (128, 64, 32, 96, 5, 1, True, False),    # 32-wide map, 8-row regions
+    (64, 128, 32, 96, 3, 1, False, False),   # 32-wide map (256-pixel blocks, 4 waves)
+    (32, 108, 64, 80, 5, 1, False, True),    # ragged 96-row tile
+    (128, 64, 32, 96, 5, 1, True, False),    # 32-wide map, two rounds
 ]
 
 
-@pytest.fixture
-def patch_on(ops):
-    """The LDS-patch conv is off by default (slower inside the concurrent iteration); these tests
-    switch it on for their duration."""
-    with ops.patch_conv(3):
-        yield
-
-
 @pytest.mark.parametrize("case", PATCH_CASES)
-def test_conv_patch_kernel(ops, patch_on, case):
+def test_conv_patch_kernel(ops, case):
+    """The split6 LDS-patch conv (the default for these shapes) against float64, and the gather
+    GEMM on the same shape (ganamd_conv_set_patch(0)) too."""
     B, Cin, H, Cout, k, mode, scaled, extra = case
     p = (k - 1) // 2
     geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
@@ -549,28 +544,31 @@ def test_conv_patch_kernel(ops, patch_on, case):
         y = torch.where(y > 0, y, al[None, :, None, None] * y)
     got = ops._conv_fwd_ex(geo, cn(x), f(w), f(sx), f(sy), 0.3, f(nz), f(ns), f(al))
     assert rel(nc(got), y) < 1e-5
-    # persistent packed weights (Parameter): the same kernel on the GEMM-order copy
+    # persistent packed weights (Parameter): the same kernel on the packed copy's bf16 planes
     wp = torch.nn.Parameter(f(w))
-    got2 = ops._conv_fwd(geo, cn(x), wp, None, f(sx), f(sy), 0.3) if not extra else None
-    if got2 is not None:
-        assert rel(nc(got2), y) < 1e-5
+    if not extra:
+        assert rel(nc(ops._conv_fwd(geo, cn(x), wp, None, f(sx), f(sy), 0.3)), y) < 1e-5
+    with ops.patch_conv(0):                      # the gather GEMM on the same (x3-packed) operand
+        assert ops.plan_info(geo, 0, scaled)["kernel"] == 0
+        assert rel(nc(ops._conv_fwd_ex(geo, cn(x), wp, f(sx), f(sy), 0.3, f(nz), f(ns), f(al))), y) < 1e-5
 
 
 DGRAD_PATCH_CASES = [
-    # B, Cin, H, Cout, k, pad mode, scaled: stride-1 dgrads whose interior takes the LDS-patch conv
-    # (zero-padded, taps reversed) and -- replication padding -- the ring the gather GEMM (s = -2)
+    # B, Cin, H, Cout, k, pad mode, scaled: stride-1 dgrads whose interior takes the split6 patch
+    # conv (zero-padded, taps reversed) and -- replication padding -- the ring the gather GEMM (s = -2)
     (32, 96, 64, 96, 5, 1, True),            # G13_5 modulated 5x5 (gy scaled by the demodulation)
-    (32, 48, 64, 40, 3, 1, False),           # 48 rows (16x16x4), K channels not a multiple of 16
-    (128, 128, 32, 128, 3, 1, False),        # D9_4 block conv on the critic's 2B batch
+    (32, 48, 64, 40, 3, 1, False),           # 48 rows (paired 16x16x32), K channels not a multiple of 16
+    (64, 96, 32, 128, 3, 1, False),          # 32-wide map
     (32, 96, 64, 80, 3, 0, False),           # zero padding: no ring
 ]
 
 
 @pytest.mark.parametrize("case", DGRAD_PATCH_CASES)
-def test_conv_patch_dgrad(ops, patch_on, case):
+def test_conv_patch_dgrad(ops, case):
     B, Cin, H, Cout, k, mode, scaled = case
     p = (k - 1) // 2
     geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
+    assert ops.plan_info(geo, 1, scaled)["kernel"] == 1
     g = torch.Generator().manual_seed(sum(case[:6]) + 7)
     xm = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
     w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64)
@@ -583,8 +581,11 @@ def test_conv_patch_dgrad(ops, patch_on, case):
     f = (lambda t: None if t is None else t.float().to(DEV))
     got = ops._conv_dgrad(geo, cn(gy), f(w), f(sy), 0.3)
     assert rel(nc(got), want) < 1e-5
-    got2 = ops._conv_dgrad(geo, cn(gy), torch.nn.Parameter(f(w)), f(sy), 0.3)   # persistent packed copy
+    wp = torch.nn.Parameter(f(w))
+    got2 = ops._conv_dgrad(geo, cn(gy), wp, f(sy), 0.3)   # persistent packed copy
     assert rel(nc(got2), want) < 1e-5
+    with ops.patch_conv(0):                      # the frame-split gather GEMM on the same copy
+        assert rel(nc(ops._conv_dgrad(geo, cn(gy), wp, f(sy), 0.3)), want) < 1e-5
 
 
 TAIL_CASES = [
@@ -772,3 +773,56 @@ def test_conv_wgrad2_two_segments(ops, case):
                                      alpha, _lib.ptr(out), 1, _lib.ptr(ws), _lib.stream())
     assert rc == 0
     assert rel(out, gw0 + ref) < 1e-5
+
+
+# ---- split6: fp32 products on the bf16 matrix cores are fp32-class ---------------------------
+# (op, B, cin, H, cout, k, stride, pad, scaled, tile kind).  Every fp32 GEMM runs as six bf16
+# products per 16 k (csrc/conv_gemm.hip split3 / mfma6_*); dropping any of the kept terms (h*l,
+# l*h, m*m: ~2^-16 relative each) would show here as ~1e-5, fp32's own rounding is ~1e-7.
+SPLIT6_CASES = [
+    ("fwd", 2, 96, 64, 96, 5, 1, 2, True, "32x32 x3 LDS body (96-row tile), x*s gather, *d epilogue"),
+    ("fwd", 2, 128, 32, 128, 3, 1, 1, False, "32x32 x3 LDS body (128-row tile)"),
+    ("fwd", 2, 48, 64, 48, 5, 1, 2, True, "48-row tile: paired 16x16x32 products"),
+    ("fwd", 2, 48, 64, 3, 5, 1, 2, False, "16-row tile (ToRGB): paired 16x16x32 products"),
+    ("dgrad", 2, 64, 64, 64, 3, 1, 1, False, "32x32 x3 body, transposed gather over the padded frame"),
+    ("dgrad", 4, 256, 16, 256, 3, 2, 1, False, "scatter-form dgrad GEMM (stride 2)"),
+    ("wgrad", 2, 48, 64, 48, 5, 1, 2, True, "48x64 wgrad tile: 16x16x16 split products"),
+    ("wgrad", 2, 96, 32, 96, 5, 1, 2, True, "96-wide wgrad tile: 16x16x16 split products"),
+    ("wgrad", 2, 128, 32, 128, 3, 1, 1, False, "32x32 wgrad tile"),
+    ("wgrad", 8, 1025, 4, 1025, 3, 1, 1, False, "96x96 wgrad tiles, the 1025-channel 4x4 block"),
+    ("fwd", 32, 96, 64, 96, 5, 1, 2, True, "split6 LDS-patch conv, 96 rows (32x32x16)"),
+    ("fwd", 32, 48, 64, 48, 5, 1, 2, True, "split6 LDS-patch conv, 48 rows (paired 16x16x32)"),
+    ("dgrad", 32, 96, 64, 96, 5, 1, 2, True, "split6 LDS-patch dgrad interior + ring GEMM"),
+]
+
+
+@pytest.mark.parametrize("case", SPLIT6_CASES, ids=[c[-1] for c in SPLIT6_CASES])
+def test_split6_fp32_class(ops, case):
+    """Each tile kind of the fp32 GEMMs against float64 at <= 1e-6 (max |err| / max |ref|) on
+    full-mantissa random operands: the split products are as accurate as fp32 MFMA."""
+    from tests._emu import emulate, max_rel
+    op, B, cin, H, cout, k, s, p, scaled, _kind = case
+    g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
+    gen = torch.Generator().manual_seed(600 + SPLIT6_CASES.index(case))
+    x = torch.randn(cin, B, H, H, generator=gen).to(DEV)
+    w = torch.nn.Parameter(torch.randn(cout, cin, k, k, generator=gen).to(DEV))
+    gy = torch.randn(cout, B, g.OH, g.OW, generator=gen).to(DEV)
+    xs = (torch.rand(cin, B, generator=gen) + 0.5).to(DEV) if scaled else None
+    ys = (torch.rand(cout, B, generator=gen) + 0.5).to(DEV) if scaled else None
+    with torch.no_grad():
+        if op == "fwd":
+            got = ops._conv_fwd(g, x, w, None, xs, ys, 0.7)
+        elif op == "dgrad":
+            got = ops._conv_dgrad(g, gy, w, ys, 0.7)
+        else:
+            got = ops._conv_wgrad(g, x, gy, xs, ys, 0.7)
+    torch.cuda.synchronize()
+    ref = emulate(op, g, x=x, w=w, gy=gy, xs=xs, ys=ys, alpha=0.7)
+    e = max_rel(got, ref)
+    e_bf = max_rel(got, emulate(op, g, x=x, w=w, gy=gy, xs=xs, ys=ys, alpha=0.7, bf16=True))
+    info = ops.plan_info(g, {"fwd": 0, "dgrad": 1}[op], scaled) if op != "wgrad" else {}
+    if "patch" in case[-1]:
+        assert info["kernel"] == 1, info
+    print(f"{case[-1]}: max rel err vs float64 {e:.2e} (vs a bf16-operand GEMM {e_bf:.2e}); plan {info}")
+    assert e <= 1e-6, e
+    assert e_bf > 1e-4                   # the operands really keep more than bf16
