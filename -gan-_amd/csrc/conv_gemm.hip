@@ -2279,10 +2279,10 @@ hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-// ---- the split6 LDS-patch conv (conv_patch.hip) ----------------------------------------------
-// bit 0: forward, bit 1: dgrad interior through the patch conv where its domain and grid fit
-// (ganamd_conv_set_patch: A/B of the two paths; default both)
-std::atomic<int> g_patch{3};
+// ---- the split6 LDS-patch conv (conv_patch.hip) and row-blocked wgrad (conv_wgrad_row.hip) ------
+// bit 0: forward, bit 1: dgrad interior through the patch conv where its domain and grid fit, bit 2:
+// weight gradients through the row-blocked kernel (ganamd_conv_set_patch: A/B; default all)
+std::atomic<int> g_patch{7};
 int patch_enabled() { return g_patch.load(std::memory_order_relaxed); }
 
 // The packed operand carries the three bf16 planes the patch conv reads (after the fp32 copy the
@@ -2516,6 +2516,17 @@ static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* 
                          ph ? d->stride : 1, ph ? d->KH : 0, ph ? d->pad : 0, pack_x3(d, op) ? 1 : 0, 0};
 }
 
+// The row-blocked split6 weight gradient (conv_wgrad_row.hip) where its domain fits: fp32 math,
+// stride-1 same convs on 32 / 64-wide maps; the split-K partial sums reduced here.
+static bool wrow_ok(const ganamd_conv_desc* d) {
+  return (patch_enabled() & 4) && d->math == GANAMD_MATH_F32 && d->KH == d->KW &&
+         ganamd_wrow::domain(d->Cout, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->transposed);
+}
+static int wrow_splits(const ganamd_conv_desc* d, int segs) {
+  int s = 1, per = 0;
+  ganamd_wrow::plan(d->Cout, d->Cin, d->B, d->H, d->W, d->KH, segs, num_cus(), &s, &per);
+  return s;
+}
 // the patch conv's arguments from the GEMM's (p: its A rows / K layout, gather source and epilogue)
 static ganamd_patch::Args patch_args(const ConvArgs& p, const float* packed, int mpad, int K, bool dgrad) {
   ganamd_patch::Args a{};
@@ -2575,7 +2586,7 @@ int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes) {
 
 int ganamd_conv_set_patch(int mask) {
   const int prev = patch_enabled();
-  if (mask >= 0) g_patch.store(mask & 3, std::memory_order_relaxed);
+  if (mask >= 0) g_patch.store(mask & 7, std::memory_order_relaxed);
   return prev;
 }
 
@@ -2666,7 +2677,11 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
     const Plan a = wgrad_plan(Mw, Jw, Kpix, T, false, bf), b = wgrad_plan(Mw, Jw, Kpix, T, true, bf);
     // ... and for the two-segment GEMM of ganamd_conv_wgrad2 (K = 2 Kpix, unscaled)
     const Plan c = wgrad_plan(Mw, Jw, 2 * Kpix, T, false, bf);
-    const int S = std::max(std::max(a.splits, b.splits), c.splits);
+    int S = std::max(std::max(a.splits, b.splits), c.splits);
+    // ... and the row-blocked kernel's (one and two segments), where it can run
+    if (d->math == GANAMD_MATH_F32 && d->KH == d->KW &&
+        ganamd_wrow::domain(d->Cout, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->transposed))
+      S = std::max(S, std::max(wrow_splits(d, 1), wrow_splits(d, 2)));
     *bytes = S > 1 ? sizeof(float) * (size_t)S * d->Cin * d->Cout * T : 0;
   } else {
     return GANAMD_EINVAL;
@@ -2949,11 +2964,50 @@ static WgradArgs wgrad_args(const ganamd_conv_desc* d, const float* x, const flo
   return p;
 }
 
+static int wgrad_row(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
+                     const float* gy_scale, const float* x2, const float* gy2, float alpha, float* gw, int accumulate,
+                     void* workspace, hipStream_t stream) {
+  ganamd_wrow::Args a{};
+  a.a = gy;
+  a.ascale = gy_scale;
+  a.x = x;
+  a.xscale = x_scale;
+  a.a2 = gy2;
+  a.x2 = x2;
+  a.M = d->Cout;
+  a.J = d->Cin;
+  a.B = d->B;
+  a.H = d->H;
+  a.W = d->W;
+  a.KK = d->KH;
+  a.replicate = d->pad_mode == GANAMD_PAD_REPLICATE;
+  a.alpha = alpha;
+  a.out = gw;
+  a.accumulate = accumulate;
+  ganamd_wrow::plan(a.M, a.J, a.B, a.H, a.W, a.KK, gy2 ? 2 : 1, num_cus(), &a.splits, &a.ks_per_split);
+  a.slab = a.splits > 1 ? static_cast<float*>(workspace) : nullptr;
+  if (a.splits > 1 && !a.slab) return GANAMD_EINVAL;
+  if (ganamd_wrow::launch(a, stream) != hipSuccess) return GANAMD_ELAUNCH;
+  if (a.splits > 1) {
+    const int numel = d->Cout * d->Cin * d->KH * d->KW;
+    if (numel % 4 == 0 && aligned16(a.slab) && aligned16(gw))
+      hipLaunchKernelGGL(wgrad_split_reduce_kernel<true>, dim3(grid1d(numel / 4)), dim3(256), 0, stream, a.slab,
+                         a.splits, numel, gw, accumulate);
+    else
+      hipLaunchKernelGGL(wgrad_split_reduce_kernel<false>, dim3(grid1d(numel)), dim3(256), 0, stream, a.slab,
+                         a.splits, numel, gw, accumulate);
+    if (hipGetLastError() != hipSuccess) return GANAMD_ELAUNCH;
+  }
+  return GANAMD_OK;
+}
+
 int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
                       const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
                       hipStream_t stream) {
   if (!desc_ok(d) || !x || !gy || !gw) return GANAMD_EINVAL;
   if ((x_scale == nullptr) != (gy_scale == nullptr)) return GANAMD_EINVAL;
+  if (wrow_ok(d))
+    return wgrad_row(d, x, gy, x_scale, gy_scale, nullptr, nullptr, alpha, gw, accumulate, workspace, stream);
   const WgradArgs p = wgrad_args(d, x, gy, x_scale, gy_scale, alpha, gw, accumulate);
   return dispatch_wgrad(p, d->KH * d->KW, static_cast<float*>(workspace), stream) == hipSuccess ? GANAMD_OK
                                                                                                 : GANAMD_ELAUNCH;
@@ -2962,6 +3016,7 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
 int ganamd_conv_wgrad2(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x2, const float* gy2,
                        float alpha, float* gw, int accumulate, void* workspace, hipStream_t stream) {
   if (!desc_ok(d) || !x || !gy || !x2 || !gy2 || !gw) return GANAMD_EINVAL;
+  if (wrow_ok(d)) return wgrad_row(d, x, gy, nullptr, nullptr, x2, gy2, alpha, gw, accumulate, workspace, stream);
   WgradArgs p = wgrad_args(d, x, gy, nullptr, nullptr, alpha, gw, accumulate);
   if (d->transposed || p.K % BKW != 0 || (long)2 * p.K >= (1L << 31) / 4) {   // two launches instead
     int rc = ganamd_conv_wgrad(d, x, gy, nullptr, nullptr, alpha, gw, accumulate, workspace, stream);

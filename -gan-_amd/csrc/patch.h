@@ -44,3 +44,34 @@ int occupancy(const Args& a);
 hipError_t launch(const Args& a, hipStream_t st);
 
 }  // namespace ganamd_patch
+
+namespace ganamd_wrow {
+
+// One launch of the row-blocked weight gradient of a stride-1 "same" K x K conv (K = 3 / 5) on
+// maps 32 / 64 wide (conv_wgrad_row.hip):
+//   out[m][j][kh][kw] (+)= alpha * sum_seg sum_n a_seg[m][n] * ascale[m][b(n)]
+//                                  * x_seg[j][b(n), oh(n) + kh - pad, ow(n) + kw - pad] * xscale[j][b(n)]
+// (replication-clamped or zero-padded source); a block owns one kernel row kh and all K taps kw
+// of it.  With splits > 1 the partial sums go to slab[split][M * J * K * K] (the caller reduces).
+struct Args {
+  const float* a;          // [M][B*H*W]
+  const float* ascale;     // [M][B] or null (both scales or neither; one segment only)
+  const float* x;          // [J][B*H*W]
+  const float* xscale;     // [J][B] or null
+  const float* a2;         // second segment (ganamd_conv_wgrad2) or null
+  const float* x2;
+  int M, J, B, H, W, KK, replicate;
+  float alpha;
+  float* out;
+  int accumulate;
+  float* slab;
+  int splits, ks_per_split;   // 32-pixel K-steps per split
+};
+
+// The kernel's domain: stride 1, same padding, K = 3 / 5, W = 32 / 64, M <= 128, not transposed.
+bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW, int transposed);
+// Split-K of a launch: splits and K-steps per split (a function of the geometry alone).
+void plan(int M, int J, int B, int H, int W, int K, int segs, int cus, int* splits, int* ks_per_split);
+hipError_t launch(const Args& a, hipStream_t st);
+
+}  // namespace ganamd_wrow

@@ -85,15 +85,18 @@ def parse():
 FAKE_GROUPS, FAKE_OVERLAP = (4, 1), False
 
 
-def fake_schedule(args, B):
-    """(overlap, real_source, allreduce, fake_groups) arguments of pipeline.Iteration."""
+def fake_schedule(args, B, world=1):
+    """(overlap, real_source, allreduce, fake_groups) arguments of pipeline.Iteration.  With N > 1
+    ranks the next fake-batch group is always made on the second stream while the current group's
+    critic steps -- and their RCCL all-reduces -- run; FAKE_OVERLAP is the N = 1
+    tuning, where there is no collective to hide."""
     if args.fake_groups:
         groups = [int(k) for k in args.fake_groups.split(",")]
     elif args.config == "wgangp" and B <= 64:
         groups = list(FAKE_GROUPS)
     else:
         groups = [1] * N_CRITIC
-    default = FAKE_OVERLAP if max(groups) > 1 else True
+    default = (FAKE_OVERLAP or world > 1) if max(groups) > 1 else True
     overlap = default if args.overlap is None else args.overlap == "on"
     return overlap, None, None, groups
 
@@ -390,7 +393,7 @@ def build(args, dev, rank, world):
         tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=rng)
     B = args.batch
     if args.config != "lazy":
-        return G, D, tr, Iteration(tr, B, N_CRITIC, world, *fake_schedule(args, B))
+        return G, D, tr, Iteration(tr, B, N_CRITIC, world, *fake_schedule(args, B, world))
     data = rng.fork(2)
 
     def real():
@@ -445,8 +448,21 @@ def main():
     ops.FlopCounter.record = None
     issued_flops = ops.FlopCounter.flops
     algo_flops, bf16_flops = ops.FlopCounter.algo_flops, ops.FlopCounter.flops_bf16
-    for _ in range(max(0, args.warmup - 1)):
+    def mem_note(i):
+        # live bytes after each eager warm-up iteration, and after a cyclic GC (what survives an
+        # iteration: DESIGN.md §2 "peak HBM vs warm-ups")
+        import gc
+        torch.cuda.synchronize()
+        a0 = torch.cuda.memory_allocated() / 2**30
+        gc.collect()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warm-up {i}: live {a0:.1f} GiB, after gc.collect {torch.cuda.memory_allocated() / 2**30:.1f} "
+                  f"GiB, peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
+    mem_note(0)
+    for i in range(max(0, args.warmup - 1)):
         iteration()
+        mem_note(i + 1)
     torch.cuda.synchronize()
     if rank == 0:
         print(f"[bench] warm-up done ({args.config}, B={B}/GPU, {world} rank(s))", file=sys.stderr, flush=True)

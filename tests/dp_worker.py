@@ -89,7 +89,10 @@ def main_graph(out):
     dev = torch.device("cuda", 0)
     G, D = make_models(gan_amd, dev)
     tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev, graph_seed(rank)))
-    it = Iteration(tr, B_GRAPH, 5, world, overlap=False, fake_groups=GRAPH_FAKE_GROUPS)   # bench's schedule
+    # bench.py's N > 1 schedule: fake groups (4, 1), the second group made on the side stream while
+    # the first group's critic steps and all-reduces run ("serial": the N = 1 order)
+    serial = len(sys.argv) > 3 and sys.argv[3] == "serial"
+    it = Iteration(tr, B_GRAPH, 5, world, overlap=not serial, fake_groups=GRAPH_FAKE_GROUPS)
     snap = snapshot(tr)
     it.eager()                     # warm-up (all-reduces included), then capture
     it.capture()

@@ -8,8 +8,9 @@ by hand, and the critic update is applied from that mean.  The all-reduced gradi
 updated critic must match at 1e-5 (gloo sums the fp32 buffers on the host: one rounding).
 
 test_dp_graph_iteration_matches_shard_mean: the bench's N > 1 GRAPH-mode path (pipeline.Iteration
-with the bench's fake-batch groups 4 + 1 from segmented-BatchNorm generator forwards, all-reduce
-between captured graphs) on two ranks equals, after
+with the bench's fake-batch groups 4 + 1 from segmented-BatchNorm generator forwards, the second
+group on the side stream during the first group's critic steps and all-reduces -- and the serial
+order -- all-reduce between captured graphs) on two ranks equals, after
 one full iteration (5 critic steps + generator step), the same iteration run here eagerly with the
 two shards one after another and their gradients averaged by hand before every optimizer step.
 
@@ -90,11 +91,12 @@ def test_dp_steps_match_shard_mean(tmp_path):
     assert _rel(got["g_grad"], g_want) < 1e-5
 
 
-def test_dp_graph_iteration_matches_shard_mean(tmp_path):
+@pytest.mark.parametrize("schedule", ["overlap", "serial"])
+def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
     out = str(tmp_path / "rank0_graph.pt")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
-           "graph"]
+           "graph", schedule]
     r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = torch.load(out, weights_only=True)

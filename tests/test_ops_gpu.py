@@ -786,9 +786,12 @@ SPLIT6_CASES = [
     ("fwd", 2, 48, 64, 3, 5, 1, 2, False, "16-row tile (ToRGB): paired 16x16x32 products"),
     ("dgrad", 2, 64, 64, 64, 3, 1, 1, False, "32x32 x3 body, transposed gather over the padded frame"),
     ("dgrad", 4, 256, 16, 256, 3, 2, 1, False, "scatter-form dgrad GEMM (stride 2)"),
-    ("wgrad", 2, 48, 64, 48, 5, 1, 2, True, "48x64 wgrad tile: 16x16x16 split products"),
-    ("wgrad", 2, 96, 32, 96, 5, 1, 2, True, "96-wide wgrad tile: 16x16x16 split products"),
-    ("wgrad", 2, 128, 32, 128, 3, 1, 1, False, "32x32 wgrad tile"),
+    ("wgrad", 2, 48, 64, 48, 5, 1, 2, True, "gather wgrad, 48x64 tile: 16x16x16 split products"),
+    ("wgrad", 2, 96, 32, 96, 5, 1, 2, True, "gather wgrad, 96-wide tile: 16x16x16 split products"),
+    ("wgrad", 2, 128, 32, 128, 3, 1, 1, False, "gather wgrad, 32x32 tile"),
+    ("wgrad", 2, 48, 64, 48, 5, 1, 2, True, "row-blocked wgrad, 48 rows (paired 16x16x32)"),
+    ("wgrad", 2, 96, 32, 96, 5, 1, 2, True, "row-blocked wgrad, 96 rows (32x32x16)"),
+    ("wgrad", 4, 128, 32, 128, 3, 1, 1, False, "row-blocked wgrad, 128 rows, split K"),
     ("wgrad", 8, 1025, 4, 1025, 3, 1, 1, False, "96x96 wgrad tiles, the 1025-channel 4x4 block"),
     ("fwd", 32, 96, 64, 96, 5, 1, 2, True, "split6 LDS-patch conv, 96 rows (32x32x16)"),
     ("fwd", 32, 48, 64, 48, 5, 1, 2, True, "split6 LDS-patch conv, 48 rows (paired 16x16x32)"),
@@ -809,7 +812,8 @@ def test_split6_fp32_class(ops, case):
     gy = torch.randn(cout, B, g.OH, g.OW, generator=gen).to(DEV)
     xs = (torch.rand(cin, B, generator=gen) + 0.5).to(DEV) if scaled else None
     ys = (torch.rand(cout, B, generator=gen) + 0.5).to(DEV) if scaled else None
-    with torch.no_grad():
+    # the gather wgrad's tile kinds on shapes the row-blocked kernel would take: mask it off (bit 2)
+    with torch.no_grad(), ops.patch_conv(3 if "gather wgrad" in case[-1] else 7):
         if op == "fwd":
             got = ops._conv_fwd(g, x, w, None, xs, ys, 0.7)
         elif op == "dgrad":
@@ -826,3 +830,43 @@ def test_split6_fp32_class(ops, case):
     print(f"{case[-1]}: max rel err vs float64 {e:.2e} (vs a bf16-operand GEMM {e_bf:.2e}); plan {info}")
     assert e <= 1e-6, e
     assert e_bf > 1e-4                   # the operands really keep more than bf16
+
+
+WGRAD_ROW_CASES = [
+    # B, Cin, H, Cout, k, pad mode, scaled: the row-blocked split6 wgrad (conv_wgrad_row.hip)
+    (16, 48, 64, 48, 5, 1, True),      # G13_5 48-channel modulated 5x5 (3 waves x 16-row blocks)
+    (8, 96, 64, 96, 5, 1, True),       # 96-channel (3 waves x 32 rows)
+    (16, 64, 64, 64, 3, 1, False),     # D9_4 64-channel block conv (2 waves)
+    (8, 128, 32, 128, 3, 1, False),    # D9_4 128-channel (4 waves)
+    (8, 40, 32, 45, 3, 0, False),      # zero padding, ragged rows / columns
+    (4, 54, 64, 102, 5, 1, True),      # 102 rows: 4 waves, ragged 32-row block
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_ROW_CASES)
+def test_conv_wgrad_row(ops, case):
+    """Row-blocked weight gradient (a block owns one kernel row and all its taps) against float64:
+    overwrite and accumulate, and equal to the gather wgrad (mask bit 2 off) at the fp32 bar."""
+    B, Cin, H, Cout, k, mode, scaled = case
+    p = (k - 1) // 2
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
+    g = torch.Generator().manual_seed(sum(case[:6]) + 11)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.zeros(Cout, Cin, k, k, dtype=torch.float64, requires_grad=True)
+    sx = torch.rand(Cin, B, generator=g, dtype=torch.float64) + 0.5 if scaled else None
+    sy = torch.rand(Cout, B, generator=g, dtype=torch.float64) + 0.5 if scaled else None
+    xm = x * sx.t()[:, :, None, None] if scaled else x
+    y = ref_conv(xm, w * 0.3, None, k, 1, p, mode)
+    if scaled:
+        y = y * sy.t()[:, :, None, None]
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    want, = torch.autograd.grad(y, w, gy)
+    f = (lambda t: None if t is None else t.float().to(DEV))
+    got = ops._conv_wgrad(geo, cn(x), cn(gy), f(sx), f(sy), 0.3)
+    assert rel(got, want) < 1e-5
+    base = torch.randn(want.shape, generator=g, dtype=torch.float64)
+    acc = base.float().to(DEV)
+    ops._conv_wgrad(geo, cn(x), cn(gy), f(sx), f(sy), 0.3, out=acc, accumulate=True)
+    assert rel(acc, base + want) < 1e-5
+    with ops.patch_conv(3):
+        assert rel(ops._conv_wgrad(geo, cn(x), cn(gy), f(sx), f(sy), 0.3), want) < 1e-5

@@ -14,6 +14,6 @@ fi
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC $2 -c $SRC -o tools/variants/$1.o
 [ -n "$3" ] && rm -f "$SRC"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o tools/variants/$1.so tools/variants/$1.o \
-  $P/build/conv_patch.hip.o $P/build/elem.hip.o $P/build/gemm_grouped.hip.o $P/build/fused.hip.o $P/build/data.hip.o $P/build/act.hip.o \
+  $P/build/conv_patch.hip.o $P/build/conv_wgrad_row.hip.o $P/build/elem.hip.o $P/build/gemm_grouped.hip.o $P/build/fused.hip.o $P/build/data.hip.o $P/build/act.hip.o \
   $P/build/rng.hip.o $P/build/critic.hip.o
 rm tools/variants/$1.o
