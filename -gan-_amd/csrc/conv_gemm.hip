@@ -49,13 +49,7 @@ constexpr int kThreads = 256;
 #define GANAMD_BK 16
 #endif
 constexpr int BK = GANAMD_BK; // conv K-step (taps x channels)
-#ifdef GANAMD_LDS128
-// LDS row stride 20 floats: 16-byte aligned rows; ds_read_b128 (lane groups {0-3,12-15,20-27},
-// ...; bank (a/4) mod 64) and ds_write_b128 (8-lane groups, mod 32) are conflict-free at it.
-constexpr int LDK = BK + 4;
-#else
 constexpr int LDK = BK + 2;   // LDS row stride in floats: 8-byte aligned, b64 reads conflict-free
-#endif
 #ifndef GANAMD_BKW
 #define GANAMD_BKW 32
 #endif
@@ -257,17 +251,6 @@ __device__ __forceinline__ int mfma_row(int lane, int r) {
 // Read this lane's 8 k-values of one 32-row fragment: rows r of the [row][k] tile, k = 8h..8h+7.
 template <int LD>
 __device__ __forceinline__ void read_frag(const float* __restrict__ base, float (&v)[8]) {
-#ifdef GANAMD_LDS128
-  if constexpr (LD % 4 == 0) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const f32x4 t = *reinterpret_cast<const f32x4*>(base + 4 * q);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
-    }
-    return;
-  }
-#endif
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const f32x2 t = *reinterpret_cast<const f32x2*>(base + 2 * q);
@@ -293,9 +276,6 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 // body (mfma_tile_x3).
 #ifndef GANAMD_SPLIT6
 #define GANAMD_SPLIT6 1
-#endif
-#ifndef GANAMD_SPLIT6_16   // the 16x16 blocks too (v_mfma_f32_16x16x16_bf16, half the bf16 rate)
-#define GANAMD_SPLIT6_16 1
 #endif
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -362,7 +342,7 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
       b[j][0] = t0[0]; b[j][1] = t0[1]; b[j][2] = t1[0]; b[j][3] = t1[1];
     }
 
-    if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT6_16) {
+    if constexpr (GANAMD_SPLIT6) {
       // 16x16x16 bf16: lane (r, q) holds A[r][4q..4q+3] -- this map.  (Pairing the products on
       // the full-rate 16x16x32 as mfma_tile_x3 does needs 8 k per lane: twice the fp32 LDS reads
       // and splits here, measured 30 % slower on the 96-wide wgrad tiles.)
@@ -421,9 +401,6 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
       for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_32(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
     return;
   }
-#ifdef GANAMD_SETPRIO
-  __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
   for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -431,9 +408,6 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
 #pragma unroll
       for (int j = 0; j < C::TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-#ifdef GANAMD_SETPRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   }
 }
 
@@ -813,28 +787,19 @@ template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
 __device__ __forceinline__ void conv_body_f32(const ConvArgs& p);
 
 
-// ---- fp32 GEMM body with split operands in LDS (GANAMD_SPLIT_LDS) ----------------------------
+// ---- fp32 GEMM body with split operands in LDS ----------------------------------------------
 // conv_body_f32's block schedule and gather, but each operand element is split ONCE -- by the
 // thread that stores it to LDS -- into three bf16 planes (h, m, l: split3); the waves read bf16
 // fragments and issue the six split products per 16 k on the bf16 matrix cores (mfma6_32 /
 // mfma6_16) instead of splitting every fragment they read.  K-step 16; 48-byte plane rows (16 k
 // + 8 pad): the fragment reads (ds_read_b128 / _b64) and the 8-k slot stores (ds_write_b128) are
 // conflict-free (MI355X_MICROARCH.md "LDS" lane groups).
-#ifndef GANAMD_SPLIT_LDS
-#define GANAMD_SPLIT_LDS 1
-#endif
-#ifndef GANAMD_X3_WIDE   // the 256-wide tiles of M <= 32 too (2 blocks per CU with 32-byte rows)
-#define GANAMD_X3_WIDE 1
-#endif
-#ifndef GANAMD_X3_SWZ
-#define GANAMD_X3_SWZ 1
-#endif
-// plane row stride (bf16 elements).  SWZ: 32-byte rows (no pad) with the two 16-byte halves of row
-// r swapped when bit 3 of r is set -- the same conflict-free fragment reads in two thirds of the LDS
-constexpr int LDH = GANAMD_X3_SWZ ? BK : BK + 8;
+// plane row stride (bf16 elements): 32-byte rows (no pad) with the two 16-byte halves of row r
+// swapped when bit 3 of r is set -- conflict-free fragment reads in two thirds of a padded layout's LDS
+constexpr int LDH = BK;
 // element offset of k-group `half` (8 k) of plane row r
 __device__ __forceinline__ int x3_off(int r, int half) {
-  return r * LDH + 8 * (GANAMD_X3_SWZ ? (half ^ ((r >> 3) & 1)) : half);
+  return r * LDH + 8 * (half ^ ((r >> 3) & 1));
 }
 
 template <class C, int PSA, int PSB>
@@ -1051,7 +1016,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD
 void conv_gemm_kernel(ConvArgs p) {
   if constexpr (BF16) {
     conv_body_bf16<BM, BN, WGM, WGN, MODE, BSCALE>(p);
-  } else if constexpr (GANAMD_SPLIT6 && GANAMD_SPLIT_LDS && (BN == 128 || GANAMD_X3_WIDE)) {
+  } else if constexpr (GANAMD_SPLIT6) {
     conv_body_x3<BM, BN, WGM, WGN, MODE, BSCALE>(p);
   } else {
     conv_body_f32<BM, BN, WGM, WGN, MODE, BSCALE>(p);
@@ -1172,25 +1137,11 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
       const int slot = tid + e * kThreads;
       if (slot < A4) {
         float* d = &As[buf][(slot / SPR) * LDK + 4 * (slot % SPR)];
-#ifdef GANAMD_LDS128
-        *reinterpret_cast<f32x4*>(d) = ra[e];
-#else
         *reinterpret_cast<f32x2*>(d) = f32x2{ra[e][0], ra[e][1]};
         *reinterpret_cast<f32x2*>(d + 2) = f32x2{ra[e][2], ra[e][3]};
-#endif
       }
     }
     float* d = &Bs[buf][b_n * LDK + b_kg * KPT];
-#ifdef GANAMD_LDS128
-    if constexpr (KPT % 4 == 0) {
-#pragma unroll
-      for (int e = 0; e < KPT; e += 4)
-        *reinterpret_cast<f32x4*>(d + e) =
-            BSCALE ? f32x4{rb[e] * rs[e], rb[e + 1] * rs[e + 1], rb[e + 2] * rs[e + 2], rb[e + 3] * rs[e + 3]}
-                   : f32x4{rb[e], rb[e + 1], rb[e + 2], rb[e + 3]};
-      return;
-    }
-#endif
 #pragma unroll
     for (int e = 0; e < KPT; e += 2)
       *reinterpret_cast<f32x2*>(d + e) =
@@ -1201,7 +1152,6 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
   zero_acc<C>(acc);
 
   Stage s0;
-#ifndef GANAMD_NO_PF2
   // two K-steps in flight: the gather for step kt+2 is issued while step kt's MFMAs run and step
   // kt+1's operands (loaded one step earlier) go to LDS -- twice the latency cover per wave
   Stage s1;
@@ -1226,20 +1176,6 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
 #pragma unroll
     for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[0], Bs[0], acc, lane, wm, wn, k0);
   }
-#else
-  gload(kt0, s0);
-  sstore(0, s0);
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) gload(kt + 1, s0);
-#pragma unroll
-    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[buf], Bs[buf], acc, lane, wm, wn, k0);
-    if (more) sstore(buf ^ 1, s0);
-    __syncthreads();
-  }
-#endif
 
   conv_epilogue<C, MODE>(p, acc, n0, m0, split, lane, wm, wn);
 }
@@ -1612,38 +1548,15 @@ __global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict
 // launch helpers
 // ------------------------------------------------------------------------------------------
 // Tuning knobs (read once): target number of workgroups the split-K heuristics aim for.
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-int wgrad_tp_enabled() {   // GANAMD_WGRAD_TP=0: one tile column set per tap (A/B)
-  static const int v = env_int("GANAMD_WGRAD_TP", 1);
-  return v;
-}
-int linear_enabled() {   // GANAMD_LINEAR=0: linears through the tiled conv GEMM (A/B)
-  static const int v = env_int("GANAMD_LINEAR", 1);
-  return v;
-}
-int splitk_enabled() {   // GANAMD_SPLITK=0 disables split-K (experiments)
-  static const int v = env_int("GANAMD_SPLITK", 1);
-  return v;
-}
-// Unused dynamic LDS per conv / wgrad block (bytes): caps the resident blocks per CU, i.e. the
-// waves per SIMD (occupancy experiments: GANAMD_CONV_LDS_PAD, GANAMD_WGRAD_LDS_PAD).
-int conv_lds_pad() {
-  static const int v = env_int("GANAMD_CONV_LDS_PAD", 0);
-  return v;
-}
-int wgrad_lds_pad() {
-  static const int v = env_int("GANAMD_WGRAD_LDS_PAD", 0);
-  return v;
-}
+// Tuning switches of the GEMM planners (the A/B experiments behind them are in profiles/r01-r03;
+// the library reads no environment): tap-packed wgrad columns, the skinny-GEMM linears, split-K,
+// no LDS padding (occupancy).
+constexpr bool wgrad_tp_enabled() { return true; }
+constexpr bool linear_enabled() { return true; }
+constexpr bool splitk_enabled() { return true; }
+constexpr int conv_lds_pad() { return 0; }
+constexpr int wgrad_lds_pad() { return 0; }
 
-
-// Split-K planning.  Splits exist only to fill the chip when the output tile grid is small;
-// each split writes its own slab (no atomics: deterministic, no contention) and a reduce
-// kernel folds the slabs.  The plan is a pure function of the geometry so the workspace query
-// and the launch agree.
 struct Plan {
   int bm, bn, splits, kt_per_split;
   int tp = 0;          // wgrad: taps packed into N (see wgrad_gemm_kernel TP)
@@ -1652,10 +1565,7 @@ struct Plan {
 // Row tile: the least padded rows per unit of tile efficiency (measured: 96-row tiles ~0.95 and
 // 64-row ~0.9 of the 128-row rate) -- e.g. M = 192 takes two 96-row tiles, not two 128-row ones
 // (256 rows, 25 % empty); a smaller tile has to beat the 128-row one by 5 %.
-int tile48() {   // GANAMD_TILE48=0: M = 33..48 on the 64-row tile (A/B)
-  static const int v = env_int("GANAMD_TILE48", 1);
-  return v;
-}
+constexpr bool tile48() { return true; }
 int conv_bm(int M) {
   if (M <= 16 && tile48()) return 16;   // ToRGB (M = 3): 16x16x4 blocks halve the empty rows
   if (M <= 32) return 32;
@@ -1666,19 +1576,10 @@ int conv_bm(int M) {
   const double bar = 0.95 * c128;   // a smaller tile only for a clear win
   return (c96 < bar && c96 <= c64) ? 96 : (c64 < bar ? 64 : 128);
 }
-int wide_tiles() {   // GANAMD_WIDE=1: 128 x 256 tiles (2 waves per SIMD) for M > 96 (A/B experiments)
-  static const int v = env_int("GANAMD_WIDE", 0);
-  return v;
-}
+constexpr bool wide_tiles() { return false; }
 int conv_bn(int bm, int) { return bm <= 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
-int tile96() {   // GANAMD_TILE96=0: wgrad keeps 128-wide tiles on J = 96, 192 (A/B)
-  static const int v = env_int("GANAMD_TILE96", 1);
-  return v;
-}
-int big96() {    // GANAMD_BIG96=0: 128x128 wgrad tiles for large M, J that pad them (A/B)
-  static const int v = env_int("GANAMD_BIG96", 1);
-  return v;
-}
+constexpr bool tile96() { return true; }
+constexpr bool big96() { return true; }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
 
 // Split-K: pure functions of the geometry (the workspace query and the launch agree).

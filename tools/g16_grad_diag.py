@@ -146,6 +146,23 @@ def compare():
         e = np.asarray([x for x, _ in lst[1:]])
         print(k, "style/demod grads: median", np.median(e), "p99", np.percentile(e, 99), "max", e.max(),
               max(lst[1:])[1])
+    # the G-step's parameter gradients (rows) against float64 truth: which tensors carry the
+    # norm-vector statistic's error (tests/_util.grad_norm_stats)
+    import json
+    from tests._util import GOLDEN, grad_norm_stats
+    truth = np.load(os.path.join(GOLDEN, "f64_g16.npz"))["g16_grads"]
+    names = [n for n, _, _ in json.load(open(os.path.join(GOLDEN, "plan.json")))["g_params"]]
+    for k, v in sides.items():
+        if "rows" not in v.files:
+            continue
+        rows = v["rows"]
+        print(k, "grad_norm_stats vs f64:", grad_norm_stats(rows, truth))
+        g, w = rows[:, 1], truth[:, 1]
+        ok = ~np.isnan(w) & ~np.isnan(g)
+        d2 = np.where(ok, (g - w) ** 2, 0.0)
+        tot = np.sqrt(np.nansum(np.where(ok, w ** 2, 0.0)))
+        for i in np.argsort(-d2)[:12]:
+            print(f"   {np.sqrt(d2[i]) / tot:.2e} of |w|  rel {abs(g[i] - w[i]) / abs(w[i]):.2e}  {names[i]}")
 
 
 if __name__ == "__main__":
