@@ -62,6 +62,8 @@ class CriticGrads(ctypes.Structure):
 COP = {k: i for i, k in enumerate(("swap", "conv", "prelu", "resample", "pmean", "sigmoid", "scale_add", "mbstd",
                                    "flatten"))}
 
+ROUTE_MAX = 8          # GANAMD_ROUTE_MAX
+
 # name -> (restype, argtypes)
 _SIGS = {
     "ganamd_version": (ctypes.c_char_p, []),
@@ -81,6 +83,8 @@ _SIGS = {
     "ganamd_gp_fwd": (c_int, [vp, c_int, c_long, c_float, c_float, c_int, vp, vp, vp, vp]),
     "ganamd_gp_bwd": (c_int, [vp, vp, vp, c_int, c_long, c_float, c_float, c_int, vp, vp]),
     "ganamd_add_prelu": (c_int, [vp, vp, vp, c_int, c_long, vp, vp]),
+    "ganamd_modconv_sd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_long, vp, vp, vp, vp]),
+    "ganamd_route_bwd": (c_int, [c_int, vp, vp, vp, c_int, c_long, vp, vp]),
     "ganamd_scale_add": (c_int, [vp, vp, vp, c_long, c_long, vp, vp]),
     "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),
     "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),

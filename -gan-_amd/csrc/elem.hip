@@ -733,6 +733,44 @@ __global__ __launch_bounds__(kNT) void plane_dot_pair_kernel(const float* __rest
   }
 }
 
+// The modulated conv's style-side gradients from its saved output y = d * conv + ns * noise
+// (generator_13_5.py:243-247, 263-265), one block per plane p = (c, b):
+//   gd[p]  = dL/dd = <gy, conv> = (<gy, y> - ns[c] <gy, noise>) / d[p]
+//   pdn[p] = <gy, noise>              (noise may be null: gd = <gy, y> / d, no pdn)
+// Both dots and the combination in double (the two terms nearly cancel when the noise dominates a
+// plane); one pass over gy, y and noise instead of a plane-dot launch plus three elementwise ones.
+__global__ __launch_bounds__(kNT) void modconv_sd_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                                                             const float* __restrict__ noise, const float* __restrict__ d,
+                                                             const float* __restrict__ ns, int B, long HW,
+                                                             float* __restrict__ gd, float* __restrict__ pdn) {
+  __shared__ double sh[4];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const long p = blockIdx.x;
+  const f4* a4 = reinterpret_cast<const f4*>(gy + p * HW);
+  const f4* c4 = reinterpret_cast<const f4*>(y + p * HW);
+  double s1 = 0.0, s2 = 0.0;
+  if (noise) {
+    const f4* d4 = reinterpret_cast<const f4*>(noise + p * HW);
+    for (long i = threadIdx.x; i < HW / 4; i += kNT) {
+      const f4 u = a4[i], v = c4[i], w = d4[i];
+      s1 += (double)u[0] * v[0] + (double)u[1] * v[1] + (double)u[2] * v[2] + (double)u[3] * v[3];
+      s2 += (double)u[0] * w[0] + (double)u[1] * w[1] + (double)u[2] * w[2] + (double)u[3] * w[3];
+    }
+    s2 = block_sum_d(s2, sh);
+  } else {
+    for (long i = threadIdx.x; i < HW / 4; i += kNT) {
+      const f4 u = a4[i], v = c4[i];
+      s1 += (double)u[0] * v[0] + (double)u[1] * v[1] + (double)u[2] * v[2] + (double)u[3] * v[3];
+    }
+  }
+  s1 = block_sum_d(s1, sh);
+  if (threadIdx.x == 0) {
+    const int c = (int)(p / B);
+    gd[p] = (float)((noise ? s1 - (double)ns[c] * s2 : s1) / (double)d[p]);
+    if (noise) pdn[p] = (float)s2;
+  }
+}
+
 __global__ void segment_sumsq_kernel(const float* __restrict__ w, long rows, int T, float* __restrict__ out) {
   for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < rows; r += (long)gridDim.x * blockDim.x) {
     const float* p = w + r * T;
@@ -1053,6 +1091,18 @@ int ganamd_plane_dot_pair(const float* a, const float* b1, const float* b2, long
       ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b1) | reinterpret_cast<uintptr_t>(b2)) & 15))
     return GANAMD_EINVAL;
   hipLaunchKernelGGL(plane_dot_pair_kernel, dim3((unsigned)planes), dim3(kNT), 0, st, a, b1, b2, HW, out1, out2);
+  return ok(hipGetLastError());
+}
+
+int ganamd_modconv_sd_bwd(const float* gy, const float* y, const float* noise, const float* d, const float* ns,
+                          int C, int B, long HW, float* gd, float* pdn, float* gns, hipStream_t st) {
+  if (!gy || !y || !d || !gd || C <= 0 || B <= 0 || HW <= 0 || HW % 4 || (noise && (!ns || !pdn)) ||
+      ((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(noise)) & 15))
+    return GANAMD_EINVAL;
+  hipLaunchKernelGGL(modconv_sd_bwd_kernel, dim3((unsigned)((long)C * B)), dim3(kNT), 0, st, gy, y, noise, d, ns, B, HW,
+                     gd, pdn);
+  if (noise && gns)   // gns[c] += sum_b pdn[c][b]  (the noise scale's gradient, into the flat buffer)
+    hipLaunchKernelGGL(reduce1_kernel, dim3((C + 255) / 256), dim3(256), 0, st, pdn, C, B, gns, 1);
   return ok(hipGetLastError());
 }
 

@@ -22,6 +22,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int kNT = 256;
+constexpr int kRouteMax = GANAMD_ROUTE_MAX;
 
 inline int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + kNT - 1) / kNT, 16384)); }
 
@@ -261,6 +262,36 @@ __global__ __launch_bounds__(kNT) void gp_backward_kernel(const float* __restric
   }
 }
 
+// route backward: gx[c][:] = sum over the parts i with lo_i <= c < hi_i of g_i[c - lo_i][:] (part
+// order), 0 where no part covers c.  The gradient of several channel-range views of one CNHW tensor
+// (the dual-path blocks' x[:d] / x[d:] / x[2d:] splits, generator_13_5.py:448-467, 496-564) in one
+// pass -- instead of one zero-filled full-size tensor per slice plus the adds that sum them.
+struct RouteParts {
+  const float* g[kRouteMax];
+  int lo[kRouteMax], hi[kRouteMax];
+  int n;
+};
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void route_bwd_kernel(RouteParts r, int C, long L, float* __restrict__ gx) {
+  const long Lv = VEC ? L / 4 : L;
+  const long n = (long)C * Lv;
+  for (long i = blockIdx.x * (long)kNT + threadIdx.x; i < n; i += (long)gridDim.x * kNT) {
+    const int c = (int)(i / Lv);
+    const long e = i - (long)c * Lv;
+    if (VEC) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < r.n; ++k)
+        if (c >= r.lo[k] && c < r.hi[k]) acc += reinterpret_cast<const f32x4*>(r.g[k])[(long)(c - r.lo[k]) * Lv + e];
+      reinterpret_cast<f32x4*>(gx)[i] = acc;
+    } else {
+      float acc = 0.f;
+      for (int k = 0; k < r.n; ++k)
+        if (c >= r.lo[k] && c < r.hi[k]) acc += r.g[k][(long)(c - r.lo[k]) * L + e];
+      gx[i] = acc;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -334,6 +365,27 @@ int ganamd_scale_add(const float* x, const float* s, const float* r, long planes
     hipLaunchKernelGGL((scale_add_kernel<true>), dim3(grid_for(n)), dim3(kNT), 0, st, x, s, r, planes, HW, y);
   else
     hipLaunchKernelGGL((scale_add_kernel<false>), dim3(grid_for(n)), dim3(kNT), 0, st, x, s, r, planes, HW, y);
+  return ok(hipGetLastError());
+}
+
+int ganamd_route_bwd(int n, const float* const* g, const int32_t* lo, const int32_t* hi, int C, long L, float* gx,
+                     hipStream_t st) {
+  if (n < 0 || n > kRouteMax || !gx || C <= 0 || L <= 0 || (n && (!g || !lo || !hi))) return GANAMD_EINVAL;
+  RouteParts r{};
+  r.n = n;
+  bool vec = (L % 4) == 0 && aligned16(gx);
+  for (int k = 0; k < n; ++k) {
+    if (!g[k] || lo[k] < 0 || hi[k] > C || lo[k] >= hi[k]) return GANAMD_EINVAL;
+    r.g[k] = g[k];
+    r.lo[k] = lo[k];
+    r.hi[k] = hi[k];
+    vec = vec && aligned16(g[k]);
+  }
+  const long m = (long)C * L / (vec ? 4 : 1);
+  if (vec)
+    hipLaunchKernelGGL((route_bwd_kernel<true>), dim3(grid_for(m)), dim3(kNT), 0, st, r, C, L, gx);
+  else
+    hipLaunchKernelGGL((route_bwd_kernel<false>), dim3(grid_for(m)), dim3(kNT), 0, st, r, C, L, gx);
   return ok(hipGetLastError());
 }
 

@@ -430,15 +430,21 @@ class BasicBlock(nn.Module):
         d = self.out_planes
         if self.is_unify:
             x = prelu(self.unify(x, w), self.activation_unify.weight)
-        x_res = torch.cat([x[:d], x[2 * d:]], 0)
-        x_tr = x[d:]
-        r3, t3 = self.rir_3((x_res, x_tr), w)
-        head = r3[:d]
-        feas_res = ops.scale_add(head, self.se_attention_residual(head), x[:d])
+        C = x.shape[0]
+        # the channel ranges of x, one view per use: x's gradient is then ONE pass (ops.route)
+        # instead of a zero-filled full-size tensor per slice plus the adds that sum them
         if self.root:
-            sc = prelu(self.shortcut(x, w), self.activation_shortcut.weight)
-            return torch.cat([feas_res, t3, sc, r3[d:]], 0)
-        return torch.cat([feas_res, t3, x[2 * d:], r3[d:]], 0)
+            x_a, x_c, x_tr, x_skip, x_sc = ops.route(x, [(0, d), (2 * d, C), (d, C), (0, d), (0, C)])
+        else:
+            x_a, x_c, x_tr, x_skip, x_tail = ops.route(x, [(0, d), (2 * d, C), (d, C), (0, d), (2 * d, C)])
+        x_res = torch.cat([x_a, x_c], 0)
+        r3, t3 = self.rir_3((x_res, x_tr), w)
+        head_se, head, r_tail = ops.route(r3, [(0, d), (0, d), (d, r3.shape[0])])
+        feas_res = ops.scale_add(head, self.se_attention_residual(head_se), x_skip)
+        if self.root:
+            sc = prelu(self.shortcut(x_sc, w), self.activation_shortcut.weight)
+            return torch.cat([feas_res, t3, sc, r_tail], 0)
+        return torch.cat([feas_res, t3, x_tail, r_tail], 0)
 
 
 class ToRGB(nn.Module):
@@ -506,16 +512,23 @@ class Tree(nn.Module):
 
     def forward(self, x, w, rgb):
         d2 = 2 * self.out_planes
-        xs = [self.prev_root(x, w)] if self.level > 1 else []
+        xs = []
+        if self.level > 1:
+            x_prev, x = ops.route(x, [(0, x.shape[0])] * 2)
+            xs.append(self.prev_root(x_prev, w))
         for i in reversed(range(1, self.level)):
             x, rgb = getattr(self, f"level_{i}")(x, w, rgb)
-            xs.append(x)
+            x_keep, x = ops.route(x, [(0, x.shape[0])] * 2)
+            xs.append(x_keep)
         for i in range(self.block_num):
             x = getattr(self, f"block_{i}")(x, w)
-            xs.append(x[:d2])
-        xs.append(x[d2:])
+            if i + 1 < self.block_num:
+                x_head, x = ops.route(x, [(0, d2), (0, x.shape[0])])
+                xs.append(x_head)
+        xs.append(x)                            # the last block's x[:d2] and x[d2:], in order
         out = self.root(torch.cat(xs, 0), w)
-        return out, self.to_rgb(out) + rgb
+        out, out_rgb = ops.route(out, [(0, out.shape[0])] * 2)
+        return out, self.to_rgb(out_rgb) + rgb
 
 
 class GeneratorBlock(nn.Module):

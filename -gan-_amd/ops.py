@@ -895,18 +895,28 @@ class ModConv(Function):
         else:
             (x, s, d, w, y), ns, noise = ctx.saved_tensors, None, None
         geo, c = ctx.geo, ctx.c
-        gns = None
-        pdn = pdy = None
-        if noise is not None and ctx.needs_input_grad[2]:
-            pair = plane_dot_pair(gy, y, noise)             # <gy, y> and <gy, noise> in one pass
-            if pair is not None:
-                pdy, pdn = pair
-        if noise is not None and pdn is None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[6]):
-            pdn = plane_dot(gy, noise)                      # [C, B]: sum_hw gy * noise
-        if pdn is not None and ctx.needs_input_grad[6]:
-            gns = pdn.sum(1)
         gy = _c(gy)
-        gx = gs = gd = gw = None
+        gx = gs = gd = gw = gns = None
+        want_d, want_ns = ctx.needs_input_grad[2], noise is not None and ctx.needs_input_grad[6]
+        if want_d or want_ns:
+            # dL/dd = <gy, conv> = (<gy, y> - ns <gy, noise>) / d and the noise scale's gradient
+            # sum_b <gy, noise> (into the flat buffer when it has one): one pass (modconv_sd_bwd)
+            tgt = flat_grad(ns) if want_ns else None
+            r = modconv_sd_bwd(gy, y, noise, d, ns, tgt)
+            if r is not None:
+                gd, pdn = r
+                if want_ns and tgt is None:
+                    gns = pdn.sum(1)
+            else:                                            # unaligned planes: plane dots
+                pdn = plane_dot(gy, noise) if noise is not None else None
+                if want_ns:
+                    gns = pdn.sum(1)
+                pdy = plane_dot(gy, y)
+                if pdn is not None:
+                    pdy = pdy - ns[:, None] * pdn
+                gd = pdy / d
+            if not want_d:
+                gd = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             gxs = _conv_dgrad(geo, gy, w, d, c)             # d/d(x*s)
             # one pass: gx = gxs * s, gs = <gxs, x> per plane (ganamd_mix_bwd with M = 1)
@@ -915,12 +925,6 @@ class ModConv(Function):
             P, HW = _planes(x)
             check(LIB.ganamd_mix_bwd(1, ptr(x), None, None, None, ptr(s), P, HW, ptr(gxs), ptr(gx), None, None, None,
                                      ptr(gs), stream()), "mix_bwd")
-        if ctx.needs_input_grad[2]:
-            if pdy is None:
-                pdy = plane_dot(gy, y)                      # y = d * conv (+ ns * noise)
-            if pdn is not None:
-                pdy = pdy - ns[:, None] * pdn
-            gd = pdy / d                                    # dL/dd = sum gy * conv
         if ctx.needs_input_grad[3]:
             tgt = flat_grad(ctx.w_arg)
             if tgt is not None:
@@ -928,6 +932,21 @@ class ModConv(Function):
             else:
                 gw = _conv_wgrad(geo, x, gy, s, d, c)
         return gx, gs, gd, gw, None, None, gns, None
+
+
+def modconv_sd_bwd(gy, y, noise, d, ns, gns_acc=None):
+    """(gd, pdn) of the modulated conv (ganamd_modconv_sd_bwd): gd = dL/dd [C, B], pdn = <gy, noise>
+    per plane (None without noise); ``gns_acc`` [C] (optional) += sum_b pdn.  None when the planes do
+    not suit the kernel's 16-byte loads."""
+    C, B, H, W = gy.shape
+    if (H * W) % 4 or any(t is not None and t.data_ptr() % 16 for t in (gy, y, noise)):
+        return None
+    gd = torch.empty((C, B), device=gy.device, dtype=torch.float32)
+    pdn = torch.empty_like(gd) if noise is not None else None
+    check(LIB.ganamd_modconv_sd_bwd(ptr(gy), ptr(_c(y)), ptr(None if noise is None else _c(noise)), ptr(_c(d)),
+                                    ptr(None if ns is None else _c(ns)), C, B, H * W, ptr(gd), ptr(pdn),
+                                    ptr(gns_acc), stream()), "modconv_sd_bwd")
+    return gd, pdn
 
 
 def demod(s, w, c, eps=1e-8):
@@ -1121,6 +1140,50 @@ class AddPReLU(Function):
 
 def add_prelu(a, b, alpha):
     return AddPReLU.apply(a, b, alpha)
+
+
+class Route(Function):
+    """Channel-range views x[lo:hi] of a CNHW tensor (each contiguous), one per use.  The backward
+    writes x's gradient in ONE pass (ganamd_route_bwd: each row the sum of the views covering it, in
+    view order; 0 where none does) -- autograd's own slice backward makes a zero-filled full-size
+    tensor per view and then adds them (the dual-path blocks of generator_13_5.py:448-467, 496-564
+    take 3-5 views of every block input).  Generator only, first order."""
+
+    @staticmethod
+    def forward(ctx, x, bounds):
+        ctx.set_materialize_grads(False)
+        ctx.bounds, ctx.shape = bounds, x.shape
+        return tuple(x[lo:hi] for lo, hi in bounds)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *gs):
+        import ctypes
+        C = ctx.shape[0]
+        L = 1
+        for s in ctx.shape[1:]:
+            L *= s
+        parts = [(_c(g), lo, hi) for g, (lo, hi) in zip(gs, ctx.bounds) if g is not None and hi > lo]
+        if not parts:
+            return None, None
+        gx = torch.empty(ctx.shape, device=parts[0][0].device, dtype=torch.float32)
+        n = len(parts)
+        arr = (ctypes.c_void_p * n)(*[ptr(g) for g, _, _ in parts])
+        lo = (ctypes.c_int32 * n)(*[lo for _, lo, _ in parts])
+        hi = (ctypes.c_int32 * n)(*[hi for _, _, hi in parts])
+        check(LIB.ganamd_route_bwd(n, arr, lo, hi, C, L, ptr(gx), stream()), "route_bwd")
+        return gx, None
+
+
+def route(x, bounds):
+    """``[x[lo:hi] for lo, hi in bounds]`` with a one-pass backward (Route); at most
+    GANAMD_ROUTE_MAX views.  Without autograd it is plain slicing."""
+    if len(bounds) > _lib.ROUTE_MAX:
+        raise _lib.GanAmdError(f"route: {len(bounds)} views > {_lib.ROUTE_MAX}")
+    bounds = tuple((int(lo), int(hi)) for lo, hi in bounds)
+    if not (torch.is_grad_enabled() and x.requires_grad):
+        return tuple(x[lo:hi] for lo, hi in bounds)
+    return Route.apply(x, bounds)
 
 
 def modconv_fused(x, s, d, w, geo, c, noise=None, noise_scale=None, act=None):

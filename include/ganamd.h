@@ -222,6 +222,14 @@ int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float
  * planes): the modulated conv backward's <gy, y> and <gy, noise> (generator_13_5.py:234-248, 265). */
 int ganamd_plane_dot_pair(const float* a, const float* b1, const float* b2, long planes, long HW, float* out1,
                           float* out2, hipStream_t stream);
+/* The modulated conv's style-side gradients from its saved output y = d * conv + ns * noise
+ * (generator_13_5.py:234-248, 263-265), planes p = (c, b) of HW floats (HW % 4 == 0, 16-byte aligned):
+ *   gd[p] = dL/dd = (<gy, y> - ns[c] * <gy, noise>) / d[p]    (dots and combination in double)
+ *   pdn[p] = <gy, noise>,  gns[c] += sum_b pdn[c][b]           (noise may be NULL: gd = <gy, y> / d;
+ *                                                               gns may be NULL)
+ * Replaces the per-sample-weight backward of F.conv2d(groups=B) with respect to the demodulation. */
+int ganamd_modconv_sd_bwd(const float* gy, const float* y, const float* noise, const float* d, const float* ns,
+                          int C, int B, long HW, float* gd, float* pdn, float* gns, hipStream_t stream);
 
 /* out[c] (=|+= with accumulate) sum_{l} a[c][l] * (b ? b[c][l] : 1) over rows of length L
  * (with b = NULL and accumulate = 1: a conv bias gradient added into the flat gradient buffer). */
@@ -278,6 +286,14 @@ int ganamd_add_prelu(const float* a, const float* b, const float* alpha, int C, 
 /* y = r + x * s[plane]  (r may be NULL: y = x * s)   (SE gating + residual, generator_13_5.py:455-466,
  * discriminator_9_4.py:158-161) */
 int ganamd_scale_add(const float* x, const float* s, const float* r, long planes, long HW, float* y,
+                     hipStream_t stream);
+/* gx[c][l] = sum over the parts k (in order) with lo[k] <= c < hi[k] of g[k][c - lo[k]][l], 0 where no
+ * part covers row c (C rows of L floats; n <= GANAMD_ROUTE_MAX parts, each g[k] [hi-lo][L]).  The
+ * backward of several channel-range views of one CNHW tensor -- the dual-path split / concat of
+ * BasicBlock and Tree (generator_13_5.py:448-467, 496-564) -- in one pass.  Replaces autograd's
+ * slice backward (a zero-filled full-size tensor per view) and the adds that sum them. */
+#define GANAMD_ROUTE_MAX 8
+int ganamd_route_bwd(int n, const float* const* g, const int32_t* lo, const int32_t* hi, int C, long L, float* gx,
                      hipStream_t stream);
 
 /* Gradient penalty on the critic's input gradient g = grad_x D(x_hat), [B][n] (n = 3*64*64):

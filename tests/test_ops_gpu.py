@@ -870,3 +870,59 @@ def test_conv_wgrad_row(ops, case):
     assert rel(acc, base + want) < 1e-5
     with ops.patch_conv(3):
         assert rel(ops._conv_wgrad(geo, cn(x), cn(gy), f(sx), f(sy), 0.3), want) < 1e-5
+
+
+@pytest.mark.parametrize("B,cin,cout,H,k,aligned", [(4, 48, 54, 16, 3, True), (3, 20, 12, 8, 5, True),
+                                                    (2, 6, 5, 5, 3, False)])
+def test_modconv_noise_grads(ops, B, cin, cout, H, k, aligned):
+    """ModConv with the StyleConv noise (generator_13_5.py:234-248, 263-265) as the generator step runs
+    it: d an input, noise_scale a parameter.  dL/dd and dL/dns come from ganamd_modconv_sd_bwd (one
+    pass, double dots) on 16-byte planes, from plane dots otherwise; float64 reference."""
+    g = torch.Generator().manual_seed(7 * cin + k)
+    x = torch.randn(B, cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    s = torch.randn(B, cin, generator=g, dtype=torch.float64, requires_grad=True)
+    d = (torch.rand(B, cout, generator=g, dtype=torch.float64) + 0.5).requires_grad_()
+    W = torch.randn(cout, cin, k, k, generator=g, dtype=torch.float64, requires_grad=True)
+    ns = (torch.rand(cout, generator=g, dtype=torch.float64) * 0.1 + 0.2).requires_grad_()
+    noise = torch.randn(B, cout, H, H, generator=g, dtype=torch.float64)
+    c = (cin * k * k) ** -0.5
+    xp = F.pad(x * s[:, :, None, None], ((k - 1) // 2,) * 4, mode="replicate")
+    y = F.conv2d(xp, W * c) * d[:, :, None, None] + ns[None, :, None, None] * noise
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    want = torch.autograd.grad(y, (x, s, d, W, ns), gy)
+    geo = ops.conv_geo(B, cin, H, H, cout, k, 1, (k - 1) // 2)
+    xa = cn(x).requires_grad_()
+    sa = s.detach().t().contiguous().float().to(DEV).requires_grad_()
+    da = d.detach().t().contiguous().float().to(DEV).requires_grad_()
+    Wa = W.detach().float().to(DEV).requires_grad_()
+    nsa = ns.detach().float().to(DEV).requires_grad_()
+    ya = ops.ModConv.apply(xa, sa, da, Wa, geo, c, nsa, cn(noise))
+    assert rel(nc(ya), y) < 1e-5
+    ya.backward(cn(gy))
+    got = (nc(xa.grad), sa.grad.t(), da.grad.t(), Wa.grad, nsa.grad)
+    for name, a, b in zip(("x", "s", "d", "W", "ns"), got, want):
+        assert rel(a, b) < 1e-5, (name, rel(a, b))
+    if aligned:       # the fused kernel ran: plane dots in double
+        r = ops.modconv_sd_bwd(cn(gy), ya.detach(), cn(noise), da.detach(), nsa.detach())
+        assert r is not None and rel(r[0].t(), want[2]) < 1e-6
+
+
+def test_route_backward(ops):
+    """ops.route views (the dual-path splits of generator_13_5.py:448-467): one-pass backward
+    (ganamd_route_bwd) == autograd's slice backward; overlapping, repeated, unused and empty views;
+    rows of L % 4 != 0 take the scalar path."""
+    for shape in ((10, 4, 8, 8), (7, 3, 3, 1)):
+        g = torch.Generator().manual_seed(shape[0])
+        x = torch.randn(shape, generator=g, dtype=torch.float64, requires_grad=True)
+        C = shape[0]
+        bounds = [(0, 3), (6, C), (3, C), (0, 3), (0, C), (C, C), (2, 5)]
+        ws = [torch.randn((hi - lo,) + shape[1:], generator=g, dtype=torch.float64) for lo, hi in bounds]
+        used = [True, True, True, True, True, False, False]
+        loss = sum((x[lo:hi] * w).sum() for (lo, hi), w, u in zip(bounds, ws, used) if u)
+        (want,) = torch.autograd.grad(loss, x)
+        xa = x.detach().float().to(DEV).requires_grad_()
+        views = ops.route(xa * 1.0, bounds)
+        assert all(v.shape[0] == hi - lo for v, (lo, hi) in zip(views, bounds))
+        la = sum((v * w.float().to(DEV)).sum() for v, w, u in zip(views, ws, used) if u)
+        la.backward()
+        assert rel(xa.grad, want) < 1e-6
