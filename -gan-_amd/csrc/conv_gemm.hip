@@ -136,11 +136,16 @@ __device__ __forceinline__ int tap_offset(const Gather& g, int oh, int ow, int k
 // go straight to the input gradient, ring positions to `ring` ([row][b][Rn], Rn ring positions
 // per image, row stride ldr) -- dropped for zero padding (ring = null), folded onto the edge
 // pixels by ring_fold_kernel for replication padding.  No frame buffer, no full fold pass.
+//
+// s = -3 (phased frame split, the stride-s dgrad): n = (b, j, i) over one phase (pqa, pqc) of the
+// padded frame, phase grid pgw wide and pgs = rows * pgw big; frame point (ps*j + pqa, ps*i + pqc),
+// then as s = -1 (the other fields are those of s = -1).
 struct OutMap {
   int s, qh, qw, OWp, ohwp, OW, OHW;
   int Rn;
   long ldr;
   float* ring;
+  int ps, pqa, pqc, pgw, pgs;
 };
 __device__ __forceinline__ long out_col(const OutMap& r, int n) {
   if (r.s == 0) return n;
@@ -170,7 +175,18 @@ __host__ __device__ __forceinline__ void ring_coord(int idx, int p, int H, int W
 __device__ __forceinline__ bool frame_target(const OutMap& r, float* y, long ldy, int n, float*& base, long& ld,
                                              long& col) {
   const int p = r.qh, H = r.qw, W = r.OW;
-  const int b = n / r.ohwp, q = n - b * r.ohwp, a = q / r.OWp, c = q - a * r.OWp;
+  int b, a, c;
+  if (r.s == -3) {
+    b = n / r.pgs;
+    const int q = n - b * r.pgs, j = q / r.pgw, i = q - j * r.pgw;
+    a = r.ps * j + r.pqa;
+    c = r.ps * i + r.pqc;
+  } else {
+    b = n / r.ohwp;
+    const int q = n - b * r.ohwp;
+    a = q / r.OWp;
+    c = q - a * r.OWp;
+  }
   if (a >= p && a < p + H && c >= p && c < p + W) {
     base = y;
     ld = ldy;
@@ -439,14 +455,30 @@ __device__ __forceinline__ void zero_acc(typename C::acc_t (&acc)[C::TM][C::TN])
 // (kh0 + s*a, kw0 + s*b) with kh0 = (qh + pad) % s (see kPhase).
 // 32-bit index arithmetic (every job's packed size and weight extent is far below 2^31, checked at
 // job creation; 64-bit divisions per element made the batched repack compute-bound).
+// Taps of phase q (qa, qc) = (q / s, q % s) of a stride-s dgrad (ps = -s): the kh = qa + s*th,
+// kw = qc + s*tw of the K x K kernel, th < ntaps(K, s, qa), tw < ntaps(K, s, qc).
+__host__ __device__ __forceinline__ int ntaps(int K, int s, int q) { return (K - q + s - 1) / s; }
+
 __device__ __forceinline__ float pack_elem(const ganamd_pack_job& j, unsigned i) {
   const unsigned nct = (unsigned)j.Ckp / BK;
   unsigned T = (unsigned)j.T, q = 0;
+  int dq = -1, dnc = 1;     // dgrad phase (ps < -1) and its tap-column count
   if (j.ps > 1) {
     T = (unsigned)(j.T / (j.ps * j.ps));
     const unsigned per = (unsigned)j.Mpad * T * (unsigned)j.Ckp;
     q = i / per;
     i -= q * per;
+  } else if (j.ps < -1) {
+    // the s*s phase blocks, each Mpad x T_q x Ckp, one after another (sum of T_q = K*K)
+    const int s = -j.ps;
+    for (dq = 0; dq < s * s - 1; ++dq) {
+      const unsigned per = (unsigned)j.Mpad * (unsigned)(ntaps(j.pk, s, dq / s) * ntaps(j.pk, s, dq % s)) *
+                           (unsigned)j.Ckp;
+      if (i < per) break;
+      i -= per;
+    }
+    dnc = ntaps(j.pk, s, dq % s);
+    T = (unsigned)(ntaps(j.pk, s, dq / s) * dnc);
   }
   const unsigned c16 = i % BK;
   const unsigned r = i / BK;
@@ -458,6 +490,10 @@ __device__ __forceinline__ float pack_elem(const ganamd_pack_job& j, unsigned i)
   if (j.ps > 1) {
     const int kk = j.pk / j.ps, qh = (int)q / j.ps, qw = (int)q - qh * j.ps;
     const int kh = (qh + j.ppad) % j.ps + j.ps * ((int)t / kk), kw = (qw + j.ppad) % j.ps + j.ps * ((int)t % kk);
+    t = (unsigned)(kh * j.pk + kw);
+  } else if (dq >= 0) {
+    const int s = -j.ps;
+    const int kh = dq / s + s * ((int)t / dnc), kw = dq % s + s * ((int)t % dnc);
     t = (unsigned)(kh * j.pk + kw);
   }
   return (m < j.M && c < j.Ck) ? j.w[(unsigned)(m * j.sm + c * j.sc) + t * (unsigned)j.st] : 0.f;
@@ -702,7 +738,13 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
     float* obase = out;
     long old = ldo, col = n;
     if (finish) {
-      if constexpr (MODE == kPhase) col = out_col(p.om, n);
+      if constexpr (MODE == kPhase) {
+        if (p.om.s == -3) {
+          if (!frame_target(p.om, p.y, p.ldy, n, obase, old, col)) continue;
+        } else {
+          col = out_col(p.om, n);
+        }
+      }
       if constexpr (MODE == kTransposed) {
         if (p.om.s == -2) {
           obase = p.om.ring;
@@ -748,7 +790,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const typename 
     float* obase = out;
     long old = ldo, col = n;
     if (finish) {
-      if constexpr (MODE == kPhase) col = out_col(p.om, n);
+      if constexpr (MODE == kPhase) {
+        if (p.om.s == -3) {
+          if (!frame_target(p.om, p.y, p.ldy, n, obase, old, col)) continue;
+        } else {
+          col = out_col(p.om, n);
+        }
+      }
       if constexpr (MODE == kTransposed) {
         if (p.om.s == -2) {
           obase = p.om.ring;
@@ -1190,7 +1238,7 @@ constexpr int kPackChunk = 4096;
 // rows of T*16 contiguous floats -- coalesced on both sides (the element-wise map reads them with a
 // stride of Cin*T floats).
 __host__ __device__ inline bool pack_transposed(const ganamd_pack_job& j) {
-  return j.ps <= 1 && j.st == 1 && j.sm == j.T && j.sc > j.sm;
+  return (j.ps == 0 || j.ps == 1) && j.st == 1 && j.sm == j.T && j.sc > j.sm;
 }
 __host__ __device__ inline int pack_rows(int T) { return T >= 256 ? 1 : 256 / T; }
 
@@ -2335,12 +2383,42 @@ static void fwd_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T)
 // gather into the padded frame would feed the MFMAs mostly zero taps there (a 4x4 map's 6x6
 // frame: 2.25x the work; a valid 3x3 conv on 5x5: 2.8x; stride 2: 4x, three taps in four
 // have the wrong parity).  The Z round trip costs (KH*KW / stride^2) x the input gradient's bytes.
+//
+// Strided convs on larger maps: dgrad as s*s phase GEMMs over the padded input frame (kPhase
+// gather of gy, OutMap s = -3).  Frame point (s*j + qa, s*i + qc) takes only the taps
+// kh = qa + s*th, kw = qc + s*tw -- ntaps(K, s, qa) x ntaps(K, s, qc) of them (3x3, s = 2: 4, 2, 2, 1),
+// summed over gy(j - th, i - tw): the algorithmic work (plus the frame ring), no tap-product buffer,
+// no fold pass; interior points are stored straight into gx, the ring folded like the stride-1
+// frame split.  Needs every phase grid the same size ((H + 2p) % s == 0) and no gy scale.
+static bool dgrad_phased(const ganamd_conv_desc* d) {
+  const int s = d->stride;
+  return !d->transposed && s > 1 && d->KH == d->KW && d->KH > 1 && d->H * d->W > 100 &&
+         (d->H + 2 * d->pad) % s == 0 && (d->W + 2 * d->pad) % s == 0 &&
+         d->OH == (d->H + 2 * d->pad - d->KH) / s + 1 && d->OW == (d->W + 2 * d->pad - d->KW) / s + 1;
+}
+
 static bool dgrad_scatter(const ganamd_conv_desc* d) {
-  return !d->transposed && d->KH * d->KW > 1 && (d->stride > 1 || d->H * d->W <= 100);
+  return !d->transposed && d->KH * d->KW > 1 && ((d->stride > 1 && !dgrad_phased(d)) || d->H * d->W <= 100);
+}
+
+// taps and grid of dgrad phase q of a phased dgrad
+static void dgrad_phase(const ganamd_conv_desc* d, int q, int* T, int* KWq, int* Hq, int* Wq) {
+  const int s = d->stride, qa = q / s, qc = q % s;
+  *KWq = ntaps(d->KW, s, qc);
+  *T = ntaps(d->KH, s, qa) * *KWq;
+  *Hq = (d->H + 2 * d->pad) / s;
+  *Wq = (d->W + 2 * d->pad) / s;
 }
 
 static void dgrad_gemm(const ganamd_conv_desc* d, int* M, int* N, int* Ck, int* T) {
   *Ck = d->Cout;
+  if (dgrad_phased(d)) {   // the largest phase (q = 0)
+    int kw, hq, wq;
+    dgrad_phase(d, 0, T, &kw, &hq, &wq);
+    *M = d->Cin;
+    *N = d->B * hq * wq;
+    return;
+  }
   if (dgrad_scatter(d)) {
     *M = d->Cin * d->KH * d->KW;
     *T = 1;
@@ -2413,8 +2491,10 @@ static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* 
   a_operand(d, op, &M, &Ck, &T, &sm, &sc);
   conv_tile(M, &bm, &bn);
   const bool ph = op == GANAMD_CONV_FWD && fwd_phased(d);
+  const bool dph = op == GANAMD_CONV_DGRAD && dgrad_phased(d);
   return ganamd_pack_job{w, packed, sm, sc, 1, M, Ck, T, (M + bm - 1) / bm * bm, (Ck + BK - 1) / BK * BK,
-                         ph ? d->stride : 1, ph ? d->KH : 0, ph ? d->pad : 0, pack_x3(d, op) ? 1 : 0, 0};
+                         ph ? d->stride : dph ? -d->stride : 1, (ph || dph) ? d->KH : 0, ph ? d->pad : 0,
+                         pack_x3(d, op) ? 1 : 0, 0};
 }
 
 // The row-blocked split6 weight gradient (conv_wgrad_row.hip) where its domain fits: fp32 math,
@@ -2459,6 +2539,7 @@ static ganamd_patch::Args patch_args(const ConvArgs& p, const float* packed, int
 // The frame-split dgrad's ring buffer (replication padding only: zero padding drops the ring)
 static size_t dgrad_pad_bytes(const ganamd_conv_desc* d) {
   if (d->transposed || d->pad == 0 || dgrad_scatter(d) || d->pad_mode != GANAMD_PAD_REPLICATE) return 0;
+  // (also the phased strided dgrad's ring)
   const size_t Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
   return sizeof(float) * (size_t)d->Cin * d->B * (Hp * Wp - (size_t)d->H * d->W);
 }
@@ -2471,7 +2552,10 @@ static int fwd_mode(const ganamd_conv_desc* d) {
   if (fwd_phased(d)) return kPhase;
   return d->transposed ? kTransposed : (d->pad_mode == GANAMD_PAD_REPLICATE ? kReplicate : kZero);
 }
-static int dgrad_mode(const ganamd_conv_desc* d) { return (dgrad_scatter(d) || d->transposed) ? kZero : kTransposed; }
+static int dgrad_mode(const ganamd_conv_desc* d) {
+  if (dgrad_phased(d)) return kPhase;
+  return (dgrad_scatter(d) || d->transposed) ? kZero : kTransposed;
+}
 static size_t slab_bytes(int M, int N, int Ck, int T, int mode, bool bf16) {
   const long a = conv_plan(M, N, Ck, T, mode, false, bf16).slab_elems, b = conv_plan(M, N, Ck, T, mode, true, bf16).slab_elems;
   return sizeof(float) * (size_t)std::max(a, b);
@@ -2565,8 +2649,14 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
     // split slabs: the frame GEMM's, or the ring-only GEMM's next to the patch conv (B x ring columns)
     const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
     const int Nring = d->B * (Hp * Wp - d->H * d->W);
-    const size_t slabs = std::max(slab_bytes(M, N, Ck, T, dgrad_mode(d), d->math == GANAMD_MATH_BF16),
-                                  Nring > 0 ? slab_bytes(M, Nring, Ck, T, kTransposed, d->math == GANAMD_MATH_BF16) : 0);
+    size_t slabs = std::max(slab_bytes(M, N, Ck, T, dgrad_mode(d), d->math == GANAMD_MATH_BF16),
+                            Nring > 0 ? slab_bytes(M, Nring, Ck, T, kTransposed, d->math == GANAMD_MATH_BF16) : 0);
+    if (dgrad_phased(d))
+      for (int q = 1; q < d->stride * d->stride; ++q) {
+        int Tq, kw, hq, wq;
+        dgrad_phase(d, q, &Tq, &kw, &hq, &wq);
+        slabs = std::max(slabs, slab_bytes(M, d->B * hq * wq, Ck, Tq, kPhase, d->math == GANAMD_MATH_BF16));
+      }
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T, pack_x3(d, op)))) + align256(dgrad_pad_bytes(d)) +
              align256(dgrad_scatter_bytes(d)) + slabs;
   } else if (op == GANAMD_CONV_WGRAD) {
@@ -2744,6 +2834,45 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   if (!d->packed_w) ws += align256(pack_bytes(M, Ck, T, pack_x3(d, GANAMD_CONV_DGRAD)));
   float* slab = reinterpret_cast<float*>(ws + align256(pad_bytes) + align256(dgrad_scatter_bytes(d)));
   const bool pre = d->packed_w != 0;
+  if (dgrad_phased(d)) {
+    if (gy_scale) return GANAMD_EINVAL;   // strided convs are unmodulated (no kPhase x scale instance)
+    // s*s phase GEMMs over the padded frame (OutMap s = -3): interior -> gx, ring -> ring buffer
+    // (replication padding; dropped for zero padding), then ring_fold_kernel
+    const int s = d->stride, Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
+    const float* wq = w;
+    if (!pre) {
+      launch_pack(pack_job(d, GANAMD_CONV_DGRAD, w, packed), stream);
+      wq = packed;
+    }
+    int bm, bn;
+    conv_tile(M, &bm, &bn);
+    const long mpad = (M + bm - 1) / bm * bm, ckp = (Ck + BK - 1) / BK * BK;
+    float* ring = pad_bytes ? reinterpret_cast<float*>(ws) : nullptr;
+    const int Rn = Hp * Wp - d->H * d->W;
+    p.ldy = (long)d->B * d->H * d->W;
+    p.y = gx;
+    long off = 0;
+    for (int q = 0; q < s * s; ++q) {
+      int Tq, KWq, Hq, Wq;
+      dgrad_phase(d, q, &Tq, &KWq, &Hq, &Wq);
+      p.w = wq + off;
+      off += mpad * Tq * ckp;
+      p.T = Tq;
+      p.N = d->B * Hq * Wq;
+      p.ohw = Hq * Wq;
+      p.g = Gather{gy, nullptr, d->Cout, d->B, d->OH, d->OW, Hq, Wq, KWq, 1, 0, kPhase, 0, 0};
+      p.om = OutMap{-3, d->pad, d->H, Wp, Hp * Wp, d->W, d->H * d->W, Rn, (long)d->B * Rn, ring,
+                    s, q / s, q % s, Wq, Hq * Wq};
+      if (dispatch_conv(p, true, nullptr, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
+    }
+    if (ring) {
+      const long planes = (long)d->Cin * d->B;
+      const long edges = (long)2 * d->W + 2 * d->H;
+      hipLaunchKernelGGL(ring_fold_kernel, dim3(grid1d(planes * edges)), dim3(256), 0, stream, ring, gx, (int)planes,
+                         d->H, d->W, d->pad);
+    }
+    return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  }
   if (dgrad_scatter(d)) {
     float* Z = reinterpret_cast<float*>(ws);
     p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, d->OH, d->OW, 1, 1, 0, kZero};

@@ -78,7 +78,7 @@ def test_python_wrappers_check_shapes(bad):
     # B, Cin, H, Cout, k, stride, pad: the census' large and small GEMMs
     (128, 128, 32, 128, 3, 1, 1), (64, 96, 64, 96, 5, 1, 2), (64, 1025, 4, 1025, 3, 1, 1),
     (64, 192, 5, 192, 3, 1, 1), (64, 1024, 16, 1024, 1, 1, 0), (64, 4100, 1, 4100, 1, 1, 0),
-    (128, 1024, 8, 1024, 3, 2, 1), (4, 5, 8, 7, 3, 1, 1)])
+    (128, 1024, 8, 1024, 3, 2, 1), (4, 5, 8, 7, 3, 1, 1), (128, 64, 64, 64, 3, 2, 1), (64, 128, 32, 128, 3, 2, 1)])
 @pytest.mark.parametrize("op", [0, 1])
 def test_conv_block_schedule(shape, op):
     """Host-side invariants of the conv GEMM block schedule (whole tiles + K-split tail)."""
@@ -93,7 +93,11 @@ def test_conv_block_schedule(shape, op):
             assert pl["S"] == 1
         # every split of a tail tile owns at least one K-step (no block leaves its slab unwritten)
         nct = -(-(geo.Cout if op == 1 else geo.Cin) // 16)
-        taps = 1 if (op == 1 and (geo.stride > 1 or h * h <= 100) and k > 1) else k * k
+        # dgrad: the scatter form (one tap) on small maps, the phased form (phase 0's taps) for strided
+        # convs on larger maps (conv_gemm.hip dgrad_scatter / dgrad_phased)
+        phased = op == 1 and s > 1 and k > 1 and h * h > 100 and (h + 2 * p) % s == 0
+        taps = 1 if (op == 1 and (s > 1 or h * h <= 100) and k > 1 and not phased) else \
+            (-(-k // s)) ** 2 if phased else k * k
         kt_total = nct * taps
         assert (pl["S"] - 1) * pl["kt_per_split"] < kt_total <= pl["S"] * pl["kt_per_split"]
         n = _lib.c_size_t(0)

@@ -57,8 +57,13 @@ CONV_CASES = [
     (4, 8, 1, 8, 3, 1, 1, 1),
     (4, 12, 4, 12, 3, 1, 1, 0),
     (2, 6, 7, 5, 5, 1, 2, 1),
-    # stride 2 takes the scatter form at every size (D9_4's 3x3 s2 downsampling convs)
+    # stride 2: the phased dgrad (s*s phase GEMMs over the padded frame) on maps > 10x10 with an
+    # even frame, the scatter form otherwise (D9_4's 3x3 s2 downsampling convs)
     (4, 24, 16, 20, 3, 2, 1, 1),
+    (2, 16, 64, 16, 3, 2, 1, 1),
+    (2, 8, 32, 12, 3, 2, 1, 0),
+    (2, 6, 12, 5, 5, 2, 2, 1),
+    (2, 5, 14, 4, 4, 2, 1, 1),
     (3, 10, 9, 7, 3, 2, 1, 0),
     (2, 8, 5, 6, 3, 2, 1, 1),
     (2, 4, 2, 4, 3, 2, 1, 1),
