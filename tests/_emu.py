@@ -18,8 +18,11 @@ import torch.nn.functional as F
 from gan_amd import _lib
 
 
+_DT = [torch.float64]     # the emulation's dtype (emulate(dtype=...)): float64, or float32 for fp32's own error
+
+
 def _bf(t, bf16):
-    return t.float().to(torch.bfloat16).double() if bf16 else t.double()
+    return t.float().to(torch.bfloat16).to(_DT[0]) if bf16 else t.to(_DT[0])
 
 
 def _scaled(t, s, bf16):
@@ -45,8 +48,18 @@ def _wshape(geo):
 
 
 def emulate(op, geo, x=None, w=None, gy=None, xs=None, ys=None, alpha=1.0, bias=None, noise=None, noise_scale=None,
-            bf16=False):
-    """float64 result (CPU): fwd / dgrad in CNHW, wgrad in the weight's layout."""
+            bf16=False, dtype=torch.float64):
+    """float64 result (CPU): fwd / dgrad in CNHW, wgrad in the weight's layout.  dtype=float32: the
+    same convolution evaluated in float32 on the host (fp32's own rounding, for error bars)."""
+    _DT[0] = dtype
+    try:
+        return _emulate(op, geo, x, w, gy, xs, ys, alpha, bias, noise, noise_scale, bf16).double()
+    finally:
+        _DT[0] = torch.float64
+
+
+def _emulate(op, geo, x, w, gy, xs, ys, alpha, bias, noise, noise_scale, bf16):
+    dt = _DT[0]
     cpu = lambda t: None if t is None else t.detach().cpu()   # noqa: E731
     x, w, gy, xs, ys, bias = map(cpu, (x, w, gy, xs, ys, bias))
     if op == "fwd":
@@ -54,20 +67,20 @@ def emulate(op, geo, x=None, w=None, gy=None, xs=None, ys=None, alpha=1.0, bias=
         y = _conv(geo, _scaled(x.reshape(geo.Cin, geo.B, geo.H, geo.W), xs, bf16), wr) * alpha
         y = y.permute(1, 0, 2, 3)
         if ys is not None:
-            y = y * ys.double()[:, :, None, None]
+            y = y * ys.to(dt)[:, :, None, None]
         if bias is not None:
-            y = y + bias.double()[:, None, None, None]
+            y = y + bias.to(dt)[:, None, None, None]
         if noise is not None:
-            y = y + noise_scale.detach().cpu().double()[:, None, None, None] * noise.detach().cpu().double()
+            y = y + noise_scale.detach().cpu().to(dt)[:, None, None, None] * noise.detach().cpu().to(dt)
         return y
     if op == "dgrad":
         wr = _bf(w.reshape(_wshape(geo)), bf16)
-        x_ = torch.zeros(geo.B, geo.Cin, geo.H, geo.W, dtype=torch.float64, requires_grad=True)
+        x_ = torch.zeros(geo.B, geo.Cin, geo.H, geo.W, dtype=dt, requires_grad=True)
         g = _scaled(gy.reshape(geo.Cout, geo.B, geo.OH, geo.OW), ys, bf16)
         gx, = torch.autograd.grad(_conv(geo, x_, wr), x_, g)
         return (gx * alpha).permute(1, 0, 2, 3)
     if op == "wgrad":
-        w_ = torch.zeros(_wshape(geo), dtype=torch.float64, requires_grad=True)
+        w_ = torch.zeros(_wshape(geo), dtype=dt, requires_grad=True)
         xin = _scaled(x.reshape(geo.Cin, geo.B, geo.H, geo.W), xs, bf16)
         g = _scaled(gy.reshape(geo.Cout, geo.B, geo.OH, geo.OW), ys, bf16)
         gw, = torch.autograd.grad(_conv(geo, xin, w_), w_, g)
