@@ -177,3 +177,49 @@ class Recorder:
         for k, (e, where) in worst.items():
             assert e <= bars[k], (k, e, where, bars[k])
         return worst
+
+
+def seq_fp32(op, geo, x=None, w=None, gy=None, xs=None, ys=None, alpha=1.0):
+    """The launch's convolution as a plain fp32 FMA loop on the device: ONE accumulator per output,
+    K = Cin*K*K (fwd) or Cout*K*K (dgrad) fp32 multiply-adds in tap order -- what a textbook fp32
+    GPU convolution does.  Its error against float64 is the yardstick of "fp32-class" for launches
+    whose outputs number in the millions (the max-error tail of any fp32 accumulation grows with
+    them).  fwd / dgrad of stride-1 replicate- or zero-padded convs; CNHW in and out."""
+    dev = (x if x is not None else gy).device
+    k, p = geo.K, geo.pad
+    W = w.detach().float().reshape(geo.Cout, geo.Cin, k, k)
+    mode = "replicate" if geo.pad_mode == _lib.PAD_REPLICATE else "constant"
+    if op == "fwd":
+        xin = x.float().reshape(geo.Cin, geo.B, geo.H, geo.W)
+        if xs is not None:
+            xin = xin * xs.float()[:, :, None, None]
+        xp = F.pad(xin, (p,) * 4, mode=mode) if p else xin
+        acc = torch.zeros(geo.Cout, geo.B, geo.OH, geo.OW, device=dev, dtype=torch.float32)
+        for ci in range(geo.Cin):
+            for kh in range(k):
+                for kw in range(k):
+                    acc.addcmul_(W[:, ci, kh, kw][:, None, None, None], xp[ci, :, kh:kh + geo.OH, kw:kw + geo.OW][None])
+        acc = acc * alpha
+        if ys is not None:
+            acc = acc * ys.float()[:, :, None, None]
+        return acc
+    if op == "dgrad":
+        g = gy.float().reshape(geo.Cout, geo.B, geo.OH, geo.OW)
+        if ys is not None:
+            g = g * ys.float()[:, :, None, None]
+        Hp, Wp = geo.H + 2 * p, geo.W + 2 * p
+        acc = torch.zeros(geo.Cin, geo.B, Hp, Wp, device=dev, dtype=torch.float32)
+        for co in range(geo.Cout):
+            for kh in range(k):
+                for kw in range(k):
+                    acc[:, :, kh:kh + geo.OH, kw:kw + geo.OW].addcmul_(W[co, :, kh, kw][:, None, None, None], g[co][None])
+        if p and mode == "replicate":      # the padding's adjoint: the ring folds onto the edge pixels
+            gx = torch.zeros(geo.Cin, geo.B, geo.H, geo.W, device=dev, dtype=torch.float32)
+            ih = torch.arange(Hp, device=dev).sub(p).clamp(0, geo.H - 1)
+            iw = torch.arange(Wp, device=dev).sub(p).clamp(0, geo.W - 1)
+            idx = (ih[:, None] * geo.W + iw[None, :]).reshape(-1)
+            gx.view(geo.Cin, geo.B, -1).index_add_(2, idx, acc.reshape(geo.Cin, geo.B, -1))
+        else:
+            gx = acc[:, :, p:p + geo.H, p:p + geo.W]
+        return gx * alpha
+    raise ValueError(op)

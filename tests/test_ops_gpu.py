@@ -836,9 +836,14 @@ def test_split6_fp32_class(ops, case):
     if "patch" in case[-1]:
         assert info["kernel"] == 1, info
     print(f"{case[-1]}: max rel err vs float64 {e:.2e} (vs a bf16-operand GEMM {e_bf:.2e}); plan {info}")
-    e32 = max_rel(emulate(op, g, x=x, w=w, gy=gy, xs=xs, ys=ys, alpha=0.7, dtype=torch.float32), ref)
-    print(f"   host float32 evaluation: {e32:.2e}")
-    assert e <= max(1e-6, 2 * e32), (e, e32)
+    if e > 1e-6:
+        # millions of outputs: compare with fp32's own error tail -- a host float32 evaluation and
+        # a plain fp32 FMA convolution on the device (one accumulator, K multiply-adds in order)
+        e32 = max_rel(emulate(op, g, x=x, w=w, gy=gy, xs=xs, ys=ys, alpha=0.7, dtype=torch.float32), ref)
+        from tests._emu import seq_fp32
+        eseq = max_rel(seq_fp32(op, g, x=x, w=w, gy=gy, xs=xs, ys=ys, alpha=0.7), ref) if op != "wgrad" else 0.0
+        print(f"   fp32 yardsticks: host float32 {e32:.2e}, sequential fp32 FMA {eseq:.2e}")
+        assert e <= max(2 * e32, eseq), (e, e32, eseq)
     assert e_bf > 1e-4                   # the operands really keep more than bf16
 
 
