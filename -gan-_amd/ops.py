@@ -92,9 +92,10 @@ PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks",
 
 
 @contextlib.contextmanager
-def patch_conv(mask: int = 3):
-    """Which stride-1 convs take the split6 LDS-patch kernel inside the block (bit 0 forward, bit 1
-    dgrad; ganamd_conv_set_patch, default 3 = both): mask 0 runs the gather GEMM instead (A/B, tests)."""
+def patch_conv(mask: int = 7):
+    """Which stride-1 convs take the split6 LDS-patch kernels inside the block (bit 0 forward, bit 1
+    dgrad, bit 2 the row-blocked weight gradient; ganamd_conv_set_patch, library default 7 = all):
+    mask 0 runs the gather GEMMs instead (A/B, tests)."""
     prev = LIB.ganamd_conv_set_patch(int(mask))
     try:
         yield

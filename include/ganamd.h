@@ -70,8 +70,9 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
  * the kernel instance). */
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info);
 /* Which stride-1 "same" convolutions on 32- / 64-wide maps take the split6 LDS-patch kernel
- * (csrc/conv_patch.hip) where its domain and grid fit: bit 0 forward, bit 1 dgrad interior
- * (default 3 = both; 0 = the gather GEMM everywhere, for A/B).  mask < 0 only queries.  Returns
+ * (csrc/conv_patch.hip) where its domain and grid fit: bit 0 forward, bit 1 dgrad interior, bit 2
+ * the row-blocked weight gradient (csrc/conv_wgrad_row.hip) (default 7 = all; 0 = the gather GEMMs
+ * everywhere, for A/B).  mask < 0 only queries.  Returns
  * the previous mask.  Plans are chosen at launch (or graph capture) time; the packed-weight
  * layout does not depend on the mask. */
 int ganamd_conv_set_patch(int mask);

@@ -1,0 +1,76 @@
+"""The B=16 generator step's mapping-network gradients (tests/test_headline_gpu.py::test_g_step_b16):
+with dL/dw fixed to its float64 truth (tools/g16_gw_f64.npy, from tools/g16_grad_diag.py cpu f64),
+the exact backward of the 12-layer mapping network gives the step's mapping gradients to 8e-5 (from
+the GPU's own dL/dw) -- yet the GPU step has 1.2e-3.  This runs the mapping network alone on the GPU
+(z of the test's Draw(421), upstream gradient = the float64 dL/dw) and prints each layer's forward
+output and parameter-gradient error against float64, next to CPU fp32."""
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import gan_amd  # noqa: E402
+from oracle import model as om  # noqa: E402
+from oracle.params import fill_module  # noqa: E402
+from tests._util import plan  # noqa: E402
+
+P = plan()
+G = gan_amd.Generator(256)
+fill_module(G, P["g_seed"])
+mp = G.block0.mapping_network
+z = om.Draw(421).randn((16, 256, 1, 1)).reshape(16, 256)
+gw = torch.from_numpy(np.load(os.path.join(REPO, "tools", "g16_gw_f64.npy")))     # [B, 256]
+
+
+def ref(dt):
+    x = z.to(dt)
+    ps, outs = [], []
+    n = mp.net
+    for i in range(0, len(n), 3):
+        lin, bn, act = n[i], n[i + 1], n[i + 2]
+        W = lin.weight.weights.detach().to(dt).clone().requires_grad_()
+        b = lin.bias.detach().to(dt).clone().requires_grad_()
+        ga = bn.weight.detach().to(dt).clone().requires_grad_()
+        be = bn.bias.detach().to(dt).clone().requires_grad_()
+        al = act.weight.detach().to(dt).clone().requires_grad_()
+        ps += [W, b, ga, be, al]
+        x = x @ (W * (1 / math.sqrt(256))).t() + b
+        mu = x.mean(0, keepdim=True)
+        var = x.var(0, unbiased=False, keepdim=True)
+        x = (x - mu) / torch.sqrt(var + 1e-5) * ga + be
+        x = torch.where(x > 0, x, al * x)
+        outs.append(x)
+    x.backward(gw.to(dt))
+    return [o.detach().double() for o in outs], [p.grad.double() for p in ps]
+
+
+o64, g64 = ref(torch.float64)
+o32, g32 = ref(torch.float32)
+mp = mp.cuda()
+x = z.t().contiguous().cuda()
+outs = []
+n = mp.net
+h = x
+for i in range(0, len(n), 3):
+    h = gan_amd.generator_13_5._lin_bn_act(n[i], n[i + 1], n[i + 2], h)
+    outs.append(h)
+h.backward(gw.t().contiguous().float().cuda())
+gg = []
+for i in range(0, len(n), 3):
+    lin, bn, act = n[i], n[i + 1], n[i + 2]
+    gg += [lin.weight.weights.grad, lin.bias.grad, bn.weight.grad, bn.bias.grad, act.weight.grad]
+
+
+def rel(a, b):
+    return float((a.double().cpu() - b).norm() / b.norm().clamp_min(1e-300))
+
+
+names = ["W", "b", "gamma", "beta", "alpha"]
+for L in range(12):
+    print(f"layer {L:2d} out: gpu {rel(outs[L].t(), o64[L]):.2e} cpu-fp32 {rel(o32[L], o64[L]):.2e}   grads: " +
+          " ".join(f"{names[k]} {rel(gg[5 * L + k], g64[5 * L + k]):.1e}/{rel(g32[5 * L + k], g64[5 * L + k]):.1e}"
+                   for k in (0, 2, 3, 4)), flush=True)
