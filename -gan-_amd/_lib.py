@@ -99,6 +99,8 @@ _SIGS = {
     "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),
     "ganamd_prelu_bwd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_long, vp, vp, vp, vp, vp]),
     "ganamd_resample2d": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int, vp]),
+    "ganamd_resample2d_add": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int,
+                                      vp, vp, vp, vp]),
     "ganamd_resample2d_sum": (c_int, [vp, vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int,
                                       vp]),
     "ganamd_plane_dot_pair": (c_int, [vp, vp, vp, c_long, c_long, vp, vp, vp]),

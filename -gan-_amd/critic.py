@@ -281,7 +281,13 @@ class Run:
         self.regions = [None] * 4       # scratch + X, G, XD, A: allocated by the sweep that fills them
         self.keep = []
         self.x = self.v = None
-        self.X, self.G, self.XD = _Values(self, 0), _Values(self, 1), _Values(self, 2)
+
+    # read access to the values (views made on access: holding _Values objects here would make a
+    # Run <-> _Values reference cycle, and a cycle keeps the run's workspace -- ~10 GiB at B = 64 --
+    # alive until the cyclic GC happens to run: peak HBM then grew with every eager iteration)
+    X = property(lambda self: _Values(self, 0))
+    G = property(lambda self: _Values(self, 1))
+    XD = property(lambda self: _Values(self, 2))
 
     def __del__(self):
         if self.plan:

@@ -795,7 +795,9 @@ __global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict
                                                          int OW,
                                                          const int32_t* __restrict__ ri, const float* __restrict__ rw,
                                                          int KR, const int32_t* __restrict__ ci,
-                                                         const float* __restrict__ cw, int KC, int ppb) {
+                                                         const float* __restrict__ cw, int KC, int ppb,
+                                                         const float* __restrict__ r, float* __restrict__ y2,
+                                                         const float* __restrict__ r2) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   extern __shared__ float lds[];
   const long p0 = (long)blockIdx.x * ppb;
@@ -851,7 +853,6 @@ __global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict
   }
   __syncthreads();
   if (!active) return;
-  float* yg = y + p0 * OH * OW;
   for (int rr = r0; rr < np * OH; rr += rstep) {
     const int pl = rr / OH, oh = rr - pl * OH;
     const float* tp = ts + pl * IH * OW + q * V;
@@ -869,11 +870,16 @@ __global__ __launch_bounds__(kNT) void resample2d_kernel(const float* __restrict
         acc[0] += w * t[0];
       }
     }
-    float* o = yg + (long)rr * OW + q * V;
-    if constexpr (V == 4)
-      *reinterpret_cast<f4*>(o) = f4{acc[0], acc[1], acc[2], acc[3]};
-    else
-      o[0] = acc[0];
+    // y = R(x) (+ r); y2 = R(x) (+ r2): the residual / fan-out outputs of ganamd_resample2d_add
+    const long oi = (p0 * OH + rr) * (long)OW + q * V;
+    if constexpr (V == 4) {
+      const f4 a = f4{acc[0], acc[1], acc[2], acc[3]};
+      *reinterpret_cast<f4*>(y + oi) = r ? a + *reinterpret_cast<const f4*>(r + oi) : a;
+      if (y2) *reinterpret_cast<f4*>(y2 + oi) = r2 ? a + *reinterpret_cast<const f4*>(r2 + oi) : a;
+    } else {
+      y[oi] = r ? acc[0] + r[oi] : acc[0];
+      if (y2) y2[oi] = r2 ? acc[0] + r2[oi] : acc[0];
+    }
   }
 }
 
@@ -907,6 +913,32 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(float* __restrict__ p, const
 inline int ok(hipError_t e) { return e == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH; }
 
 }  // namespace
+
+static int resample_launch(const float* x, const float* x2, long planes, int IH, int IW, float* y, int OH, int OW,
+                           const int32_t* ri, const float* rw, int KR, const int32_t* ci, const float* cw, int KC,
+                           const float* r, float* y2, const float* r2, hipStream_t st) {
+  if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;
+  // planes per workgroup: ~2K staged inputs but <= ~8K outputs (an upsampling adjoint such as
+  // pool5's 5x5 -> 64x64 would otherwise pack 81 planes, 330K outputs, into each of a few dozen
+  // workgroups), LDS <= 48 KB (3 workgroups per CU)
+  const int V = (OW % 4 == 0 && ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(r) |
+                                  reinterpret_cast<uintptr_t>(y2) | reinterpret_cast<uintptr_t>(r2)) & 15) == 0) ? 4 : 1;
+  if (OW / V > kNT || IH <= 0 || IW <= 0 || OH <= 0 || OW <= 0) return GANAMD_EINVAL;
+  const long per_plane = (long)IH * IW + (long)IH * OW;
+  const long tab = 2L * ((long)OW * KC + (long)OH * KR) + 8;   // tables + alignment slack (floats)
+  if ((per_plane + tab) * 4 > 48 * 1024) return GANAMD_EINVAL;
+  int ppb = (int)std::max<long>(1, std::min<long>(2048 / ((long)IH * IW), 8192 / ((long)OH * OW)));
+  ppb = (int)std::min<long>(ppb, (48 * 1024 / 4 - tab) / per_plane);
+  const long blocks = (planes + ppb - 1) / ppb;
+  const size_t bytes = 4 * (size_t)(align4(ppb * IH * IW) + align4(ppb * IH * OW) + 2 * (OW * KC + OH * KR));
+  if (V == 4)
+    hipLaunchKernelGGL(resample2d_kernel<4>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, x2, planes, IH, IW, y,
+                       OH, OW, ri, rw, KR, ci, cw, KC, ppb, r, y2, r2);
+  else
+    hipLaunchKernelGGL(resample2d_kernel<1>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, x2, planes, IH, IW, y,
+                       OH, OW, ri, rw, KR, ci, cw, KC, ppb, r, y2, r2);
+  return ok(hipGetLastError());
+}
 
 extern "C" {
 
@@ -1049,27 +1081,15 @@ int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int
 int ganamd_resample2d_sum(const float* x, const float* x2, long planes, int IH, int IW, float* y, int OH, int OW,
                           const int32_t* ri, const float* rw, int KR, const int32_t* ci, const float* cw, int KC,
                           hipStream_t st) {
-  if (!x || !y || !ri || !rw || !ci || !cw || planes <= 0 || KR <= 0 || KC <= 0) return GANAMD_EINVAL;
-  // planes per workgroup: ~2K staged inputs but <= ~8K outputs (an upsampling adjoint such as
-  // pool5's 5x5 -> 64x64 would otherwise pack 81 planes, 330K outputs, into each of a few dozen
-  // workgroups), LDS <= 48 KB (3 workgroups per CU)
-  const int V = (OW % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 4 : 1;
-  if (OW / V > kNT || IH <= 0 || IW <= 0 || OH <= 0 || OW <= 0) return GANAMD_EINVAL;
-  const long per_plane = (long)IH * IW + (long)IH * OW;
-  const long tab = 2L * ((long)OW * KC + (long)OH * KR) + 8;   // tables + alignment slack (floats)
-  if ((per_plane + tab) * 4 > 48 * 1024) return GANAMD_EINVAL;
-  int ppb = (int)std::max<long>(1, std::min<long>(2048 / ((long)IH * IW), 8192 / ((long)OH * OW)));
-  ppb = (int)std::min<long>(ppb, (48 * 1024 / 4 - tab) / per_plane);
-  const long blocks = (planes + ppb - 1) / ppb;
-  const size_t bytes = 4 * (size_t)(align4(ppb * IH * IW) + align4(ppb * IH * OW) + 2 * (OW * KC + OH * KR));
-  if (V == 4)
-    hipLaunchKernelGGL(resample2d_kernel<4>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, x2, planes, IH, IW, y,
-                       OH, OW, ri, rw, KR, ci, cw, KC, ppb);
-  else
-    hipLaunchKernelGGL(resample2d_kernel<1>, dim3((unsigned)blocks), dim3(kNT), bytes, st, x, x2, planes, IH, IW, y,
-                       OH, OW, ri, rw, KR, ci, cw, KC, ppb);
-  return ok(hipGetLastError());
+  return resample_launch(x, x2, planes, IH, IW, y, OH, OW, ri, rw, KR, ci, cw, KC, nullptr, nullptr, nullptr, st);
 }
+
+int ganamd_resample2d_add(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
+                          const float* rw, int KR, const int32_t* ci, const float* cw, int KC, const float* r,
+                          float* y2, const float* r2, hipStream_t st) {
+  return resample_launch(x, nullptr, planes, IH, IW, y, OH, OW, ri, rw, KR, ci, cw, KC, r, y2, r2, st);
+}
+
 
 int ganamd_plane_dot(const float* a, const float* b, long planes, long HW, float scale, float* out, hipStream_t st) {
   if (!a || !out || planes <= 0 || HW <= 0) return GANAMD_EINVAL;

@@ -84,6 +84,18 @@ def _mix(feas, att):
     return ops.mix(feas, att)
 
 
+def _sk_mix(attn, feas):
+    """SK mixing of the branches by their attention (generator_13_5.py:80-89, 165-170, 196-202).  With
+    autograd on two branches of an SKAttention_conv the pool of the branch sum and the branches'
+    pass-through to the mix are one op (ops.pool_sum_fanout): the sum is never stored and each branch's
+    gradient (mix + pool) is written in one pass."""
+    if len(feas) == 2 and isinstance(attn, SKAttention_conv) and torch.is_grad_enabled() and \
+            (feas[0].requires_grad or feas[1].requires_grad):
+        t, f0, f1 = ops.pool_sum_fanout(feas[0], feas[1], "pool5")
+        return _mix([f0, f1], attn.head(t))
+    return _mix(feas, attn(feas))
+
+
 def _heads(attn, z):
     if not torch.is_grad_enabled():   # each head's last linear writes its slice of [M, C, B] (no stack copy)
         out = torch.empty((attn.M,) + tuple(z.shape), device=z.device, dtype=torch.float32)
@@ -125,6 +137,10 @@ class SKAttention_conv(nn.Module):
                 u = u + f
             assert u.shape[2] >= 8
             t = ops.resample(u, "pool5")
+        return self.head(t)
+
+    def head(self, t):
+        """The attention from the pooled branch sum t [C, B, 5, 5]."""
         cm = self.conv_main
         t = _conv_bn_act(cm[0], cm[1], cm[2], t)
         t = _conv_bn_act(cm[3], cm[4], cm[5], t)
@@ -185,7 +201,7 @@ class SKConvT(nn.Module):
         geo = ops.convT_geo(B, C, H, W, C, 4, 2, 1)
         a = bn_act(ops.conv2d(x, self.convT.weight, self.convT.bias, geo, 1.0), self.bn, self.activation_convT)
         b = ops.resample(x, "up2_smooth")
-        return _mix([a, b], self.sk_attention([a, b]))
+        return _sk_mix(self.sk_attention, [a, b])
 
 
 class SKConv(nn.Module):
@@ -204,7 +220,7 @@ class SKConv(nn.Module):
     def forward(self, x):
         feas = [_conv_bn_act(getattr(self, f"conv_{i}"), getattr(self, f"BatchNorm_{i}"),
                              getattr(self, f"nonlinear_{i}"), x) for i in range(self.M)]
-        return _mix(feas, self.sk_attention(feas))
+        return _sk_mix(self.sk_attention, feas)
 
 
 class MappingNetwork(nn.Module):
@@ -296,7 +312,7 @@ class SKStyleConv(nn.Module):
         # the k3 / k5 branches run in order on the current stream: the stream-level parallelism
         # is ResnetInit's four StyleBlocks (ops.Branches does not nest)
         feas = [getattr(self, f"conv_{i}")(x, w, getattr(self, f"nonlinear_{i}").weight) for i in range(self.M)]
-        return _mix(feas, self.sk_attention(feas))
+        return _sk_mix(self.sk_attention, feas)
 
 
 class StyleBlock(nn.Module):

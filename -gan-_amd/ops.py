@@ -811,6 +811,51 @@ def resample_sum(x1, x2, kind: str):
     return y
 
 
+class PoolSumFanout(Function):
+    """(t, f0', f1') = (R(f0 + f1), f0, f1): SK attention's pool of the branch sum
+    (generator_13_5.py:82-84) with the branches passed through as aliases for the mixing that
+    follows.  Forward: one resample of the sum formed while staging (ganamd_resample2d_sum) -- the sum
+    is never stored.  Backward: each branch's gradient = R^T(g_t) + its mixing gradient, both written
+    by ONE launch (ganamd_resample2d_add) -- instead of an R^T(g_t) tensor plus one add per branch."""
+
+    @staticmethod
+    def forward(ctx, f0, f1, table):
+        ctx.set_materialize_grads(False)
+        ctx.table, ctx.shape = table, f0.shape
+        idx, w, k = table.fwd
+        f0, f1 = _c(f0), _c(f1)
+        C, B = f0.shape[0], f0.shape[1]
+        t = torch.empty((C, B, table.n_out, table.n_out), device=f0.device, dtype=torch.float32)
+        check(LIB.ganamd_resample2d_sum(ptr(f0), ptr(f1), C * B, table.n_in, table.n_in, ptr(t), table.n_out,
+                                        table.n_out, iptr(idx), ptr(w), k, iptr(idx), ptr(w), k, stream()),
+              "resample2d_sum")
+        return t, f0.view_as(f0), f1.view_as(f1)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gt, g0, g1):
+        if gt is None:
+            return g0, g1, None
+        tab = ctx.table
+        idx, w, k = tab.adj
+        C, B = ctx.shape[0], ctx.shape[1]
+        y0 = torch.empty(ctx.shape, device=gt.device, dtype=torch.float32)
+        y1 = torch.empty_like(y0)
+        check(LIB.ganamd_resample2d_add(ptr(_c(gt)), C * B, tab.n_out, tab.n_out, ptr(y0), tab.n_in, tab.n_in,
+                                        iptr(idx), ptr(w), k, iptr(idx), ptr(w), k,
+                                        ptr(None if g0 is None else _c(g0)), ptr(y1),
+                                        ptr(None if g1 is None else _c(g1)), stream()), "resample2d_add")
+        return y0, y1, None
+
+
+def pool_sum_fanout(f0, f1, kind: str):
+    """(resample(f0 + f1, kind), f0, f1) with the fused backward of PoolSumFanout (autograd form of
+    resample_sum for two branches that are also used elsewhere)."""
+    if f0.shape != f1.shape or f0.dim() != 4 or f0.shape[2] != f0.shape[3]:
+        raise _lib.GanAmdError(f"pool_sum_fanout: {tuple(f0.shape)} vs {tuple(f1.shape)}")
+    return PoolSumFanout.apply(f0, f1, tables.table(kind, f0.shape[2], f0.device))
+
+
 # ------------------------------------------------------------------------------------------
 # per-plane mean (AdaptiveAvgPool2d(1)) -> [C, B]
 # ------------------------------------------------------------------------------------------

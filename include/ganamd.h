@@ -213,6 +213,13 @@ int ganamd_resample2d(const float* x, long planes, int IH, int IW, float* y, int
 int ganamd_resample2d_sum(const float* x, const float* x2, long planes, int IH, int IW, float* y, int OH, int OW,
                           const int32_t* ri, const float* rw, int KR, const int32_t* ci, const float* cw, int KC,
                           hipStream_t stream);
+/* y = R(x) + r and (y2 non-NULL) y2 = R(x) + r2 (r / r2 may be NULL: no residual), R the resampling
+ * above.  The backward of SK attention's pool of the branch sum (generator_13_5.py:82-84): each branch
+ * receives R^T(g_t) on top of the gradient its mixing use gave it -- one pass, no R^T(g_t) tensor and
+ * no adds. */
+int ganamd_resample2d_add(const float* x, long planes, int IH, int IW, float* y, int OH, int OW, const int32_t* ri,
+                          const float* rw, int KR, const int32_t* ci, const float* cw, int KC, const float* r,
+                          float* y2, const float* r2, hipStream_t stream);
 
 /* out[p] = scale * sum_{hw} a[p][hw] * (b ? b[p][hw] : 1)   (planes of HW elements).
  * Replaces AdaptiveAvgPool2d(1) (generator_13_5.py:52,362) and the per-(channel,sample)

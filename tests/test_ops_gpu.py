@@ -941,3 +941,27 @@ def test_route_backward(ops):
         la = sum((v * w.float().to(DEV)).sum() for v, w, u in zip(views, ws, used) if u)
         la.backward()
         assert rel(xa.grad, want) < 1e-6
+
+
+@pytest.mark.parametrize("C,B,n", [(6, 4, 16), (3, 2, 8), (5, 3, 64)])
+def test_pool_sum_fanout(ops, C, B, n):
+    """SK attention's pool of the branch sum with the branches passed on to the mix
+    (generator_13_5.py:82-89): t = pool5(f0 + f1) and each branch's gradient = pool5^T(g_t) + its own
+    (ganamd_resample2d_sum / ganamd_resample2d_add) == autograd through the float64 reference;
+    also with one branch's pass-through unused."""
+    g = torch.Generator().manual_seed(C * n)
+    f0 = torch.randn(B, C, n, n, generator=g, dtype=torch.float64, requires_grad=True)
+    f1 = torch.randn(B, C, n, n, generator=g, dtype=torch.float64, requires_grad=True)
+    wt = torch.randn(B, C, 5, 5, generator=g, dtype=torch.float64)
+    w0 = torch.randn(B, C, n, n, generator=g, dtype=torch.float64)
+    w1 = torch.randn(B, C, n, n, generator=g, dtype=torch.float64)
+    for use1 in (True, False):
+        t = F.adaptive_avg_pool2d(f0 + f1, 5)
+        loss = (t * wt).sum() + (f0 * w0).sum() + ((f1 * w1).sum() if use1 else 0)
+        g0, g1 = torch.autograd.grad(loss, (f0, f1))
+        a0, a1 = cn(f0).requires_grad_(), cn(f1).requires_grad_()
+        ta, b0, b1 = ops.pool_sum_fanout(a0, a1, "pool5")
+        assert rel(nc(ta), t) < 1e-5
+        la = (ta * cn(wt)).sum() + (b0 * cn(w0)).sum() + ((b1 * cn(w1)).sum() if use1 else 0)
+        la.backward()
+        assert rel(nc(a0.grad), g0) < 1e-5 and rel(nc(a1.grad), g1) < 1e-5
