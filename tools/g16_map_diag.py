@@ -43,13 +43,14 @@ def ref(dt):
         var = x.var(0, unbiased=False, keepdim=True)
         x = (x - mu) / torch.sqrt(var + 1e-5) * ga + be
         x = torch.where(x > 0, x, al * x)
+        x.retain_grad()
         outs.append(x)
     x.backward(gw.to(dt))
-    return [o.detach().double() for o in outs], [p.grad.double() for p in ps]
+    return [o.detach().double() for o in outs], [p.grad.double() for p in ps], [o.grad.double() for o in outs]
 
 
-o64, g64 = ref(torch.float64)
-o32, g32 = ref(torch.float32)
+o64, g64, h64 = ref(torch.float64)
+o32, g32, h32 = ref(torch.float32)
 mp = mp.cuda()
 x = z.t().contiguous().cuda()
 outs = []
@@ -57,6 +58,7 @@ n = mp.net
 h = x
 for i in range(0, len(n), 3):
     h = gan_amd.generator_13_5._lin_bn_act(n[i], n[i + 1], n[i + 2], h)
+    h.retain_grad()
     outs.append(h)
 h.backward(gw.t().contiguous().float().cuda())
 gg = []
@@ -73,4 +75,22 @@ names = ["W", "b", "gamma", "beta", "alpha"]
 for L in range(12):
     print(f"layer {L:2d} out: gpu {rel(outs[L].t(), o64[L]):.2e} cpu-fp32 {rel(o32[L], o64[L]):.2e}   grads: " +
           " ".join(f"{names[k]} {rel(gg[5 * L + k], g64[5 * L + k]):.1e}/{rel(g32[5 * L + k], g64[5 * L + k]):.1e}"
-                   for k in (0, 2, 3, 4)), flush=True)
+                   for k in (0, 2, 3, 4)) +
+          f"   d/d(out): gpu {rel(outs[L].grad.t(), h64[L]):.1e} cpu-fp32 {rel(h32[L], h64[L]):.1e}", flush=True)
+
+# the last layer's backward step by step on the GPU ops (layer 11: BN+PReLU backward, then the linear's
+# input gradient), against float64 on the same saved values
+L = 11
+lin, bn, act = n[3 * L], n[3 * L + 1], n[3 * L + 2]
+x_in = outs[L - 1].detach().double().cpu().t()          # [B, 256] the layer's input (GPU forward)
+W = lin.weight.weights.detach().double().cpu() / 16.0
+pre = x_in @ W.t() + lin.bias.detach().double().cpu()
+mu, var = pre.mean(0), pre.var(0, unbiased=False)
+xh = (pre - mu) / torch.sqrt(var + 1e-5)
+z = xh * bn.weight.detach().double().cpu() + bn.bias.detach().double().cpu()
+g = gw.double() * torch.where(z > 0, torch.ones_like(z), act.weight.detach().double().cpu().expand_as(z))
+gbn = (g - g.mean(0) - xh * (g * xh).mean(0)) * bn.weight.detach().double().cpu() / torch.sqrt(var + 1e-5)
+gin = gbn @ W
+print("layer 11 input-gradient from its own saved values: gpu", f"{rel(outs[L - 1].grad.t(), gin):.2e}")
+print("batch-mean of d/d(out 10) (float64 truth, gpu):", float(h64[10].mean(0).abs().max()),
+      float(outs[10].grad.t().double().cpu().mean(0).abs().max()), "scale", float(h64[10].abs().max()))
