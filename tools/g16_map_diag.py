@@ -94,3 +94,28 @@ gin = gbn @ W
 print("layer 11 input-gradient from its own saved values: gpu", f"{rel(outs[L - 1].grad.t(), gin):.2e}")
 print("batch-mean of d/d(out 10) (float64 truth, gpu):", float(h64[10].mean(0).abs().max()),
       float(outs[10].grad.t().double().cpu().mean(0).abs().max()), "scale", float(h64[10].abs().max()))
+
+# layer 10's BatchNorm + PReLU backward ALONE on the GPU (fresh autograd graph, the GPU's own input and
+# upstream gradient) -- does the kernel reproduce the chain's error?
+L = 10
+lin, bn, act = n[3 * L], n[3 * L + 1], n[3 * L + 2]
+for p_ in (bn.weight, bn.bias, act.weight):
+    p_.grad = None
+with torch.no_grad():
+    pre10 = lin(outs[L - 1].detach())
+pre10 = pre10.detach().clone().requires_grad_()
+y10 = gan_amd.ops.bn_act(pre10, bn, act)
+gy10 = outs[L].grad.detach().clone()
+y10.backward(gy10)
+pre64 = pre10.detach().double().cpu().t().clone().requires_grad_()
+mu, var = pre64.mean(0), pre64.var(0, unbiased=False)
+ga64 = bn.weight.detach().double().cpu().clone().requires_grad_()
+be64 = bn.bias.detach().double().cpu().clone().requires_grad_()
+al64 = act.weight.detach().double().cpu().clone().requires_grad_()
+zz = (pre64 - mu) / torch.sqrt(var + 1e-5) * ga64 + be64
+yy = torch.where(zz > 0, zz, al64 * zz)
+yy.backward(gy10.double().cpu().t())
+print("layer 10 BN+PReLU backward alone:  gx", f"{rel(pre10.grad.t(), pre64.grad):.2e}", " gamma",
+      f"{rel(bn.weight.grad, ga64.grad):.2e}", " beta", f"{rel(bn.bias.grad, be64.grad):.2e}", " alpha",
+      f"{rel(act.weight.grad, al64.grad):.2e}")
+print("forward y10 vs chain out 10:", f"{rel(y10.t(), outs[L].detach().double().cpu().t()):.2e}")
