@@ -249,8 +249,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
     const bool more = cc + 1 < nct;
     f32x4 pv[UPT];
     int kh = 0, kw = 0;
-#pragma unroll 1
-    for (int t = 0; t < T; t += 2) {
+    auto tap_pair = [&](int t) {
       // two taps per iteration: register double buffer fa[0] / fa[1] without dynamic indexing
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -280,6 +279,17 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
 #pragma unroll
           for (int q = 0; q < 3; ++q) fa[0][i][q] = fa[1][i][q];
       }
+    };
+    // the tap loop: fully unrolled where the registers allow it (48-row blocks, the 4-wave W = 32
+    // blocks: the taps' index math, weight prefetch and patch stores resolve at compile time and the
+    // next tap's fragment reads can be scheduled under the current tap's products); the 8-wave 96-row
+    // blocks spill when unrolled and keep a loop of two taps
+    if constexpr (BM == 48 || NW == 4) {
+#pragma unroll
+      for (int t = 0; t < T; t += 2) tap_pair(t);
+    } else {
+#pragma unroll 1
+      for (int t = 0; t < T; t += 2) tap_pair(t);
     }
     if (more) __syncthreads();       // chunk cc + 1's patch is complete; chunk cc's buffer is free
   }
