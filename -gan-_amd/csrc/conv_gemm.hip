@@ -845,9 +845,12 @@ __device__ __forceinline__ void conv_body_f32(const ConvArgs& p);
 // plane row stride (bf16 elements): 32-byte rows (no pad) with the two 16-byte halves of row r
 // swapped when bit 3 of r is set -- conflict-free fragment reads in two thirds of a padded layout's LDS
 constexpr int LDH = BK;
-// element offset of k-group `half` (8 k) of plane row r
+// element offset of k-group `half` (8 k) of plane row r.  32x32 fragments (a ds_read_b128 lane
+// group on one half) need the halves swapped on odd 8-row groups; 16x16 fragments (lanes 16-31 on
+// the other half of lanes 0-15's rows) the plain layout (2-way conflicts otherwise; conv_patch.hip poff)
+template <int MB>
 __device__ __forceinline__ int x3_off(int r, int half) {
-  return r * LDH + 8 * (half ^ ((r >> 3) & 1));
+  return MB == 32 ? r * LDH + 8 * (half ^ ((r >> 3) & 1)) : r * LDH + 8 * half;
 }
 
 template <class C, int PSA, int PSB>
@@ -864,14 +867,14 @@ __device__ __forceinline__ void mfma_tile_x3(const unsigned short* __restrict__ 
     bf16x8 a[C::TM][3], b[C::TN][3];
 #pragma unroll
     for (int i = 0; i < C::TM; ++i) {
-      const int o = x3_off((wm * C::TM + i) * 16 + r, hf);
+      const int o = x3_off<16>((wm * C::TM + i) * 16 + r, hf);
       a[i][0] = *reinterpret_cast<const bf16x8*>(&As[a0 + o]);   // (h | m)
       a[i][1] = *reinterpret_cast<const bf16x8*>(&As[a1 + o]);   // (h | l)
       a[i][2] = *reinterpret_cast<const bf16x8*>(&As[a2 + o]);   // (m | h)
     }
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) {
-      const int o = x3_off((wn * C::TN + j) * 16 + r, hf);
+      const int o = x3_off<16>((wn * C::TN + j) * 16 + r, hf);
       b[j][0] = *reinterpret_cast<const bf16x8*>(&Bs[b0 + o]);   // (h | h)
       b[j][1] = *reinterpret_cast<const bf16x8*>(&Bs[b1 + o]);   // (m | h)
       b[j][2] = *reinterpret_cast<const bf16x8*>(&Bs[b2 + o]);   // (m | l)
@@ -890,12 +893,12 @@ __device__ __forceinline__ void mfma_tile_x3(const unsigned short* __restrict__ 
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        a[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl * PSA + x3_off((wm * C::TM + i) * 32 + r, h)]);
+        a[i][pl] = *reinterpret_cast<const bf16x8*>(&As[pl * PSA + x3_off<32>((wm * C::TM + i) * 32 + r, h)]);
 #pragma unroll
     for (int j = 0; j < C::TN; ++j)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        b[j][pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl * PSB + x3_off((wn * C::TN + j) * 32 + r, h)]);
+        b[j][pl] = *reinterpret_cast<const bf16x8*>(&Bs[pl * PSB + x3_off<32>((wn * C::TN + j) * 32 + r, h)]);
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
@@ -1024,7 +1027,7 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
       if (slot < SA) {
         const float v[8] = {S.ra[e][0][0], S.ra[e][0][1], S.ra[e][0][2], S.ra[e][0][3],
                             S.ra[e][1][0], S.ra[e][1][1], S.ra[e][1][2], S.ra[e][1][3]};
-        store_split8<PSA>(&As[buf][x3_off(slot / SPR, slot % SPR)], v);
+        store_split8<PSA>(&As[buf][x3_off<C::MB>(slot / SPR, slot % SPR)], v);
       }
     }
 #pragma unroll
@@ -1032,7 +1035,7 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
       float v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = BSCALE ? S.rb[e + q] * S.rs[e + q] : S.rb[e + q];
-      store_split8<PSB>(&Bs[buf][x3_off(b_n, (b_kg * KPT + e) / 8)], v);
+      store_split8<PSB>(&Bs[buf][x3_off<C::MB>(b_n, (b_kg * KPT + e) / 8)], v);
     }
   };
 

@@ -77,10 +77,15 @@ __device__ __forceinline__ void split4(const f32x4& x, bf16x4& h, bf16x4& m, bf1
   for (int e = 0; e < 4; ++e) l[e] = (__bf16)r[e];
 }
 
-// element offset of 8-channel half `half` of patch position `pos` in one plane: 32-byte rows, the
-// two 16-byte halves swapped on odd 8-position groups (conflict-free ds_read_b128 fragment reads
-// of 16 consecutive positions at any start)
-__device__ __forceinline__ int poff(int pos, int half) { return pos * 16 + 8 * (half ^ ((pos >> 3) & 1)); }
+// element offset of 8-channel half `half` of patch position `pos` in one plane: 32-byte rows.  The
+// ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) see 16 consecutive positions:
+// 32x32 fragments (all lanes of a group on one half) need the two 16-byte halves swapped on odd
+// 8-position groups; 16x16 fragments (lanes 16-31 on the other half of lanes 0-15's positions) need
+// the plain layout -- each is conflict-free at any start position, the other one 2-way.
+template <int MB>
+__device__ __forceinline__ int poff(int pos, int half) {
+  return MB == 32 ? pos * 16 + 8 * (half ^ ((pos >> 3) & 1)) : pos * 16 + 8 * half;
+}
 
 template <int MB>
 __device__ __forceinline__ int mfma_row(int lane, int r) {
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
       }
       bf16x4 h, m, l;
       split4(v, h, m, l);
-      const int o = poff(pos, cg >> 1) + 4 * (cg & 1);
+      const int o = poff<MB>(pos, cg >> 1) + 4 * (cg & 1);
       *reinterpret_cast<bf16x4*>(&P[o]) = h;
       *reinterpret_cast<bf16x4*>(&P[PS + o]) = m;
       *reinterpret_cast<bf16x4*>(&P[2 * PS + o]) = l;
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   auto b_read = [&](const unsigned short* P, int toff, bf16x8 (&fb)[TN][3]) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int o = poff(posb[j] + toff, fhalf);
+      const int o = poff<MB>(posb[j] + toff, fhalf);
       fb[j][0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
       fb[j][1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
       fb[j][2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);

@@ -71,9 +71,13 @@ __device__ __forceinline__ void split3(const float* x, V& h, V& m, V& l) {
   for (int e = 0; e < N; ++e) l[e] = (__bf16)r[e];
 }
 
-// A planes: rows of 16 k (one 16-pixel substep), the two 8-k halves swapped on odd 8-row groups
-// (conflict-free ds_read_b128 fragments, as conv_gemm.hip x3_off)
-__device__ __forceinline__ int aoff(int r, int half) { return r * 16 + 8 * (half ^ ((r >> 3) & 1)); }
+// A planes: rows of 16 k (one 16-pixel substep); 32-row blocks: the two 8-k halves swapped on odd
+// 8-row groups, 16-row blocks (lanes 16-31 on the other half of lanes 0-15's rows): plain -- each
+// conflict-free for its ds_read_b128 lane groups (conv_patch.hip poff)
+template <int MB>
+__device__ __forceinline__ int aoff(int r, int half) {
+  return MB == 32 ? r * 16 + 8 * (half ^ ((r >> 3) & 1)) : r * 16 + 8 * half;
+}
 
 // elements kw .. kw + 7 of a 16-element bf16 window w (8 dwords): a static shift
 template <int KW>
@@ -108,7 +112,9 @@ template <int MB, int NW, int TN, int KK, bool SCALED>
 __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   constexpr int NT = 64 * NW, BM = NW * MB, BJ = TN * MB, PAD = (KK - 1) / 2, T = KK * KK;
   constexpr int SEG = KS + KK - 1;                 // staged input columns
-  constexpr int LDB = 56;                          // B row stride (bf16): 112 B, conflict-free windows
+  // B row stride (bf16): 112 B (7 16-byte chunks) for 32-row blocks, 96 B (6 chunks) for 16-row
+  // blocks -- the row strides whose window reads are conflict-free for each fragment's lane groups
+  constexpr int LDB = MB == 32 ? 56 : 48;
   constexpr int PSA = BM * 16, ABUF = 2 * 3 * PSA; // two 16-pixel substeps x three planes
   constexpr int PSB = BJ * LDB, BBUF = 3 * PSB;
   constexpr int AU = BM * 4, AUT = (AU + NT - 1) / NT;   // A units: 8 pixels of one row
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
           for (int q = 0; q < 8; ++q) v[q] *= S.sa[e];
         bf16x8 h, m, l;
         split3<8>(v, h, m, l);
-        unsigned short* d = &As[buf][(g >> 1) * 3 * PSA + aoff(r, g & 1)];
+        unsigned short* d = &As[buf][(g >> 1) * 3 * PSA + aoff<MB>(r, g & 1)];
         *reinterpret_cast<bf16x8*>(d) = h;
         *reinterpret_cast<bf16x8*>(d + PSA) = m;
         *reinterpret_cast<bf16x8*>(d + 2 * PSA) = l;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   auto compute = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {                      // two 16-pixel substeps
-      const unsigned short* A = &As[buf][s * 3 * PSA + aoff(arow, fh)];
+      const unsigned short* A = &As[buf][s * 3 * PSA + aoff<MB>(arow, fh)];
       bf16x8 a[3];
       if constexpr (MB == 32) {
 #pragma unroll
