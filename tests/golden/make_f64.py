@@ -299,7 +299,55 @@ def headline_main(trials=3):
     # box's host inside the test, with bars from the B=16 spread above.
 
 
+# The B=16 generator step's float64 forward puts ONE PReLU input on the kink: G13_5's main mapping
+# network, layer 10 (block0.mapping_network.net.32), sample 11, channel 209, z = 5.24e-7 (|z| ~ 0.8
+# elsewhere).  An fp32 evaluation's ~1e-6 forward rounding decides which branch of the PReLU it
+# takes, and the two branches' gradients differ by 2.8e-2 in that layer's BatchNorm bias (1.5e-2
+# below it): a perturbation of that layer's pre-activations by 1e-6 (relative, random) moves the
+# float64 step to exactly the GPU's numbers (tools/g16_map_diag.py; no such jump at 1e-7).  The
+# reference's own fp32 run lands on the float64 side, the GPU's on the other.  kink_main() adds the
+# float64 truth of the OTHER branch (same step, that one PReLU derivative taken as the slope).
+KINK = ("block0.mapping_network.net.32", 11, 209)
+
+
+def kink_main():
+    torch.set_num_threads(os.cpu_count() or 8)
+    pl = plan()
+    gnames = [n for n, _, _ in pl["g_params"]]
+    name, kb, kc = KINK
+    orig = om.prelu
+    seen = {}
+
+    def prelu(P, pre, x, c):
+        if pre != name:
+            return orig(P, pre, x, c)
+        a = P(f"{pre}.weight", (c,), "prelu")
+        seen["z"] = float(x[kb, kc])
+        mask = x > 0
+        mask[kb, kc] = ~mask[kb, kc]                    # the other branch at the kink element
+        return torch.where(mask, x, a * x)
+
+    om.prelu = prelu
+    smooth32 = om._SMOOTH
+    om._SMOOTH = smooth32.to(DT)
+    GP, DP = params64(pl["g_params"], pl["g_seed"]), params64(pl["d_params"], pl["d_seed"])
+    _gen, g_loss = om.WGANGP(GP, DP).generator_trainstep(16, Draw64(421))
+    om._SMOOTH, om.prelu = smooth32, orig
+    rows = grad_rows(GP, gnames)
+    path = os.path.join(HERE, "f64_g16.npz")
+    cur = dict(np.load(path))
+    cur["g16_grads_kink"] = rows
+    cur["g16_loss_kink"] = np.asarray([float(g_loss.detach())])
+    cur["kink_z"] = np.asarray([seen["z"]])
+    print("kink branch: z", seen["z"], "loss", float(g_loss.detach()), "vs", float(cur["g16_loss"][0]),
+          "grads vs the float64 branch", grad_norm_stats(rows, cur["g16_grads"]), flush=True)
+    np.savez_compressed(path, **cur)
+
+
 if __name__ == "__main__":
+    if "--kink" in sys.argv:
+        kink_main()
+        sys.exit(0)
     if "--headline" in sys.argv:
         headline_main()
         sys.exit(0)

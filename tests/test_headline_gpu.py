@@ -79,19 +79,24 @@ def test_g_step_b16(gan, P):
     assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-3
     has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
     assert (has == fx["has_grad"]).all()
-    got = grad_norm_stats(rows, t64["g16_grads"])
+    # The float64 forward of this step puts ONE PReLU input on the kink (make_f64.py KINK: the main
+    # mapping network's layer 10, sample 11, channel 209, z = 5.2e-7 against |z| ~ 0.8): fp32's
+    # ~1e-6 forward rounding picks the branch, and the two branches' gradients differ by 2.8e-2 in
+    # that layer's BatchNorm bias and ~1.5e-2 in every mapping layer below it (a 1e-6 perturbation
+    # of the float64 forward there reproduces the GPU's numbers exactly; tools/g16_map_diag.py).  The
+    # reference's fp32 run lands on the float64 branch, this build's on the other: the GPU is held
+    # to the float64 truth of the branch it took (g16_grads_kink: the same step with that one PReLU
+    # derivative taken as the slope), at the same bars -- 2x the reference's / the fp32 spread.
+    sides = {"float64 branch": t64["g16_grads"]}
+    if "g16_grads_kink" in t64.files:
+        sides["other branch at the kink"] = t64["g16_grads_kink"]
+    stats = {k: grad_norm_stats(rows, v) for k, v in sides.items()}
+    side = min(stats, key=lambda k: stats[k][3])
+    got = stats[side]
     worst = np.maximum(t64["ref_g16_stats"], t64["g16_fp32_spread"].max(axis=0))
     bars = [2 * w + 1e-5 for w in worst]
-    # The norm-vector statistic is dominated by the 12-layer main mapping network, whose gradient
-    # is dL/dw summed over the 519 style MLPs and then pushed through 12 BatchNorm1d layers over 16
-    # samples: an O(1e-4) difference in dL/dw grows ~10x there.  The network itself is exact to
-    # 1e-6 on the GPU (tools/mapping_diag.py: GPU 1.2e-6 vs CPU fp32 2.1e-6 against float64); the
-    # build's dL/dw differs from the reference's by its fp32 summation order.  Measured: 5.9e-4
-    # here (the reference's own 7.6e-5; at B=64, where BatchNorm over 64 samples conditions the
-    # chain, 3.4e-5 against the oracle).  The bar for that one statistic is the north-star 1e-3.
-    bars[3] = max(bars[3], 1e-3)
-    print("G-step B=16 vs f64 truth", got, "reference", t64["ref_g16_stats"], "bars", bars)
-    assert all(g <= b for g, b in zip(got, bars)), (got, bars)
+    print("G-step B=16 vs f64 truth", stats, "->", side, "reference", t64["ref_g16_stats"], "bars", bars)
+    assert all(g <= b for g, b in zip(got, bars)), (side, got, bars)
     assert rel_err([loss], t64["g16_loss"]) <= 2 * max(float(t64["ref_g16_loss_err"]),
                                                        float(t64["g16_loss_fp32_spread"].max())) + 1e-6
 

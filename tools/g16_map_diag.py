@@ -119,3 +119,40 @@ print("layer 10 BN+PReLU backward alone:  gx", f"{rel(pre10.grad.t(), pre64.grad
       f"{rel(bn.weight.grad, ga64.grad):.2e}", " beta", f"{rel(bn.bias.grad, be64.grad):.2e}", " alpha",
       f"{rel(act.weight.grad, al64.grad):.2e}")
 print("forward y10 vs chain out 10:", f"{rel(y10.t(), outs[L].detach().double().cpu().t()):.2e}")
+
+# the chain again, keeping the graph: are BNAct 10's saved tensors intact after the backward?
+for p_ in mp.parameters():
+    p_.grad = None
+h = x
+outs2 = []
+for i in range(0, len(n), 3):
+    h = gan_amd.generator_13_5._lin_bn_act(n[i], n[i + 1], n[i + 2], h)
+    outs2.append(h)
+node = outs2[10].grad_fn
+saved_before = [t.detach().clone() for t in node.saved_tensors]
+h.backward(gw.t().contiguous().float().cuda(), retain_graph=True)
+torch.cuda.synchronize()
+saved_after = [t.detach().clone() for t in node.saved_tensors]
+for k, (a_, b_) in enumerate(zip(saved_before, saved_after)):
+    if a_ is not None:
+        print(f"BNAct 10 saved tensor {k} {tuple(a_.shape)}: changed by the backward: {float((a_ - b_).abs().max()):.3e}")
+print("chain again: gamma10", f"{rel(n[31].weight.grad, g64[5 * 10 + 2]):.2e}", "beta10", f"{rel(n[31].bias.grad, g64[5 * 10 + 3]):.2e}")
+
+# what BNAct 10's backward actually receives in the chain (a pre-hook on its node)
+for p_ in mp.parameters():
+    p_.grad = None
+h = x
+outs3 = []
+for i in range(0, len(n), 3):
+    h = gan_amd.generator_13_5._lin_bn_act(n[i], n[i + 1], n[i + 2], h)
+    outs3.append(h)
+got_in = {}
+outs3[10].grad_fn.register_prehook(lambda go: got_in.__setitem__("gy", [None if g is None else g.detach().clone() for g in go]))
+outs3[10].register_hook(lambda g: got_in.__setitem__("tensor_hook", g.detach().clone()))
+h.backward(gw.t().contiguous().float().cuda())
+torch.cuda.synchronize()
+gys = got_in["gy"]
+print("BNAct 10 receives", len(gys), "grads:", [None if g is None else (tuple(g.shape), g.is_contiguous()) for g in gys])
+print("  vs tensor hook:", f"{float((gys[0] - got_in['tensor_hook']).abs().max()):.3e}",
+      " vs float64 truth:", f"{rel(gys[0].t(), h64[10]):.2e}")
+print("chain with hooks: gamma10", f"{rel(n[31].weight.grad, g64[5 * 10 + 2]):.2e}")
