@@ -169,10 +169,37 @@ class Train(CheckpointMixin):
         pred_r, pred_f = pred[:b_size], pred[b_size:]
         real_loss = -torch.mean(pred_r)
         fake_loss = torch.mean(pred_f)
+        # The penalty's forward and input-gradient sweep (wgangp.py:34-54) depend on the two batches
+        # only: they run on a second HIP stream concurrently with the first-order backward -- the
+        # critic's small-map layers leave most of the chip idle, two sweeps fill it.  The fork comes
+        # after the first-order forward has been issued (its plan set-up packs every weight copy the
+        # penalty's sweeps read).  gp.backward() -- the tangent + adjoint sweeps, on the second
+        # stream -- is ordered after the first-order backward by autograd's stream semantics, so the
+        # weight gradients accumulate in the reference's order.
+        side = self._penalty_stream()
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
         (real_loss + fake_loss).backward()
-        gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
+        if side is None:
+            gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
         gp.backward()
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
         return real_loss, fake_loss, gp
+
+    def _penalty_stream(self):
+        """The second stream of discriminator_backward (one per caller stream, so a captured graph and
+        an eager step never share it), or None off the GPU / for critics other than D9_4."""
+        if self.device.type != "cuda" or not isinstance(self.discriminator, Discriminator):
+            return None
+        cur = torch.cuda.current_stream()
+        streams = self.__dict__.setdefault("_gp_streams", {})
+        s = streams.get(cur.cuda_stream)
+        if s is None:
+            s = streams[cur.cuda_stream] = torch.cuda.Stream(device=self.device)
+        return s
 
     def train(self, checkpoints=True):
         """Epoch loop of train/wgangp.py:73-95: resume from ``checkpoint/.pth`` if present, one
