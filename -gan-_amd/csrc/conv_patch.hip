@@ -25,7 +25,8 @@
 // (48 rows): three full-rate v_mfma_f32_16x16x32_bf16 on pairs of products.
 //
 // Block: NW waves, NPIX pixels (whole rows) of ONE image, all BM (<= 96) output channels of a row
-// tile; wave w owns pixels [w * NPIX / NW, (w + 1) * NPIX / NW).  W = 64: 512 pixels, 8 waves;
+// tile; wave w owns pixels [w * NPIX / NW, (w + 1) * NPIX / NW) of all rows -- or, 96-row blocks at
+// W = 64 (12 waves), rows 32 (w % 3) .. +31 of pixels 128 (w / 3) .. +127.  W = 64: 512 pixels, 8 waves;
 // W = 32: 256 pixels, 4 waves.  LDS: 2 x 3 planes x positions x 16 channels x 2 B (W = 64, K = 5:
 // 153 KiB) -- one block per CU.
 
@@ -95,9 +96,12 @@ __device__ __forceinline__ int mfma_row(int lane, int r) {
 template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
 __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int NT = 64 * NW;
-  constexpr int PW = NPIX / NW;                             // pixels per wave
+  // waves along M: 12-wave 96-row blocks split the rows three ways (32 rows x 128 pixels per wave: a
+  // third of the weight fragments per wave, 3 waves per SIMD); otherwise every wave owns all rows
+  constexpr int WM = (BM == 96 && NW == 12) ? 3 : 1, WN = NW / WM;
+  constexpr int PW = NPIX / WN;                             // pixels per wave
   constexpr int MB = (BM % 32 == 0) ? 32 : 16;              // MFMA block edge (48 rows: 16)
-  constexpr int TM = BM / MB, TN = PW / MB, NR = MB == 32 ? 16 : 4;
+  constexpr int TM = BM / (MB * WM), TN = PW / MB, NR = MB == 32 ? 16 : 4;
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
   constexpr int TH = NPIX / TW, PAD = (KK - 1) / 2, T = KK * KK;
   constexpr int PWD = TW + KK - 1, NPOS = (TH + KK - 1) * PWD;
@@ -105,10 +109,11 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int BUF = 3 * PS;
   constexpr int NU = NPOS * 4, UPT = (NU + NT - 1) / NT;    // staging units: 4 channels at one position
   constexpr int kStoreTap = T > 4 ? 3 : T - 1;
-  static_assert(TN >= 1 && TM * MB == BM && TN * MB == PW, "tile");
+  static_assert(TN >= 1 && TM * MB * WM == BM && TN * MB == PW && WM * WN == NW, "tile");
   __shared__ __attribute__((aligned(16))) unsigned short Ps[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wrow = (wv % WM) * TM * MB, wcol = (wv / WM) * PW;   // this wave's rows / pixels
   const int H = p.H, HW = H * TW;
   const int gy = (p.M + BM - 1) / BM;
   const int ty = blockIdx.x % gy, reg = blockIdx.x / gy;
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   const int fhi = MB == 32 ? 0 : (lane >> 5);
   int a_row[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) a_row[i] = 2 * (((m0 + i * MB + fr) * nct * T) * 16 + 8 * fhalf);   // bytes
+  for (int i = 0; i < TM; ++i) a_row[i] = 2 * (((m0 + wrow + i * MB + fr) * nct * T) * 16 + 8 * fhalf);   // bytes
   const int pl0 = MB == 32 ? 0 : (fhi ? 1 : 0), pl1 = MB == 32 ? 1 : (fhi ? 2 : 0), pl2 = MB == 32 ? 2 : (fhi ? 0 : 1);
   const int wpb = 2 * p.wplane;                             // plane stride in bytes
   auto a_load = [&](int kt, bf16x8 (&fa)[TM][3]) {
@@ -190,7 +195,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   int posb[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int q = wv * PW + j * MB + fr;
+    const int q = wcol + j * MB + fr;
     posb[j] = (q / TW) * PWD + q % TW;
   }
   const int bq0 = 0, bq1 = MB == 32 ? 1 : (fhi ? 0 : 1), bq2 = MB == 32 ? 2 : (fhi ? 2 : 1);
@@ -298,13 +303,13 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   const long n_img = (long)b * HW + (long)oh0 * TW;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int q = wv * PW + j * MB + (lane & (MB - 1));
+    const int q = wcol + j * MB + (lane & (MB - 1));
     const long col = n_img + (q / TW) * TW + q % TW;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        const int m = m0 + i * MB + mfma_row<MB>(lane, r);
+        const int m = m0 + wrow + i * MB + mfma_row<MB>(lane, r);
         if (m >= p.M) continue;
         float v = p.alpha * acc[i][j][r];
         if (p.oscale) v *= p.oscale[m * p.B + b];
@@ -333,10 +338,11 @@ int occ_of() {
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
   if (a.W == 64) {
-    if (occ) *occ = occ_of<BM, 8, 512, KK, 64, BSCALE, DGRAD>();
+    constexpr int NW = BM == 96 ? 12 : 8;
+    if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
-      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, 8, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)), dim3(512),
-                         0, st, a);
+      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),
+                         dim3(64 * NW), 0, st, a);
   } else {
     if (occ) *occ = occ_of<BM, 4, 256, KK, 32, BSCALE, DGRAD>();
     if (!dry)
