@@ -514,21 +514,40 @@ class _PenaltyFn(Function):
         return (None,) * 6
 
 
+def penalty_sweeps(D, x_hat):
+    """The part of the gradient penalty that depends on x_hat only: the forward and the input-gradient
+    sweep of D at x_hat (no autograd node; may run on a second stream, see wgangp.Train)."""
+    run = Run(program_of(D), 1)
+    x_hat = x_hat.detach().contiguous()
+    run.forward(x_hat)
+    seed = torch.ones((1, x_hat.shape[0]), device=x_hat.device, dtype=torch.float32)
+    return run, run.backward(seed, params=False, need_input=True)
+
+
+def adopt(run, g, stream):
+    """Tensors of ``penalty_sweeps`` made on another stream are used on ``stream`` from here on (the
+    caching allocator must not hand their memory out before that stream's use is done)."""
+    if torch.cuda.is_current_stream_capturing():      # a captured graph's pool frees nothing mid-replay
+        return
+    for t in [g, run.x] + [r for r in run.regions if r is not None]:
+        t.record_stream(stream)
+
+
+def penalty_value(D, run, g, center=1.0, lam=1.0, mode=0):
+    """The fused penalty on the input gradient g of ``penalty_sweeps``; its ``.backward()`` runs the
+    double backward (tangent + adjoint sweeps) on the stream current at that call."""
+    params = [p for p in program_of(D).params if p.requires_grad]
+    if not params or not torch.is_grad_enabled():
+        return _penalty(g, center, lam, mode)[0]
+    return _PenaltyFn.apply(params[0], run, g, center, lam, mode)
+
+
 def gradient_penalty(D, x_hat, center=1.0, lam=1.0, mode=0):
     """lam * mean_b (||grad_x sum D(x_hat)||_b - center)^2 (train/wgangp.py:34-54) -- or, mode 1,
     lam * mean_b ||.||^2 (R1/R2) -- with forward, input-gradient backward and the fused penalty
     run now; ``.backward()`` on the result runs the double backward (tangent + adjoint sweeps)."""
-    prog = program_of(D)
-    run = Run(prog, 1)
-    x_hat = x_hat.detach().contiguous()
-    run.forward(x_hat)
-    B = x_hat.shape[0]
-    seed = torch.ones((1, B), device=x_hat.device, dtype=torch.float32)
-    g = run.backward(seed, params=False, need_input=True)
-    params = [p for p in prog.params if p.requires_grad]
-    if not params or not torch.is_grad_enabled():
-        return _penalty(g, center, lam, mode)[0]
-    return _PenaltyFn.apply(params[0], run, g, center, lam, mode)
+    run, g = penalty_sweeps(D, x_hat)
+    return penalty_value(D, run, g, center, lam, mode)
 
 
 def regularised_step(D, x, segments, loss_w, specs):

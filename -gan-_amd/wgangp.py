@@ -173,20 +173,25 @@ class Train(CheckpointMixin):
         # only: they run on a second HIP stream concurrently with the first-order backward -- the
         # critic's small-map layers leave most of the chip idle, two sweeps fill it.  The fork comes
         # after the first-order forward has been issued (its plan set-up packs every weight copy the
-        # penalty's sweeps read).  gp.backward() -- the tangent + adjoint sweeps, on the second
-        # stream -- is ordered after the first-order backward by autograd's stream semantics, so the
-        # weight gradients accumulate in the reference's order.
+        # penalty's sweeps read); the penalty value, its autograd node and its double backward
+        # (tangent + adjoint sweeps) are made on this stream after the join, so the weight gradients
+        # accumulate in the reference's order and no autograd node lives on the second stream.
         side = self._penalty_stream()
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
-        (real_loss + fake_loss).backward()
         if side is None:
+            (real_loss + fake_loss).backward()
             gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
+        else:
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                eps = self.rng.rand((b_size,)).view(b_size, 1, 1, 1)
+                x_interp = ((1 - eps) * images + eps * gen_imgs.detach()).detach()
+                run, g = critic.penalty_sweeps(self.discriminator, x_interp)
+            (real_loss + fake_loss).backward()
+            cur.wait_stream(side)
+            critic.adopt(run, g, cur)
+            gp = 10 * critic.penalty_value(self.discriminator, run, g, 1.0, 1.0, 0)
         gp.backward()
-        if side is not None:
-            torch.cuda.current_stream().wait_stream(side)
         return real_loss, fake_loss, gp
 
     def _penalty_stream(self):
