@@ -1,6 +1,7 @@
 #!/bin/bash
-# HBM traffic of bench.py's roofline kernel -- the dominant one, conv_gemm_kernel<96,128,1,4,1,true,false>:
-# G13_5's modulated conv fwd 96->96 5x5 64x64 at bench.py's whole-tile probe batch -- from rocprofv3 PMC counters, one counter per pass (FETCH_SIZE and
+# HBM traffic of bench.py's roofline kernel -- the dominant one, the split6 LDS-patch conv
+# conv_patch_x3_kernel<96,...,5,64,true,false>: G13_5's modulated conv fwd 96->96 5x5 64x64 at bench.py's
+# whole-tile probe batch -- from rocprofv3 PMC counters, one counter per pass (FETCH_SIZE and
 # WRITE_SIZE cannot share a pass on gfx950).  FETCH_SIZE is doubled (gfx950 reports half the bytes
 # of wide coalesced reads: MI355X_MICROARCH.md, HBM section).  Writes profiles/roofline_traffic.json.
 set -e
@@ -18,7 +19,7 @@ B = int(os.environ["B"])
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(f"/tmp/pmc_{c}/**/*counter_collection.csv", recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if "conv_gemm_kernel<96, 128, 1, 4, 1, true, false>" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(f)) if "conv_patch_x3_kernel<96, " in r["Kernel_Name"]]
     per = {}
     for r in rows:
         per.setdefault(r["Dispatch_Id"], 0.0)
@@ -28,7 +29,7 @@ fetch_b = 2 * vals["FETCH_SIZE"] * 1024
 write_b = vals["WRITE_SIZE"] * 1024
 # x read + packed W read + x/y scales + y write, once
 alg = 4 * (96 * B * 64 * 64 + 96 * 96 * 25 + 2 * 96 * B + 96 * B * 64 * 64)
-out = {"kernel": "conv_gemm_kernel<96,128,...,true,false>", "batch": B,
+out = {"kernel": "conv_patch_x3_kernel<96,...,5,64,true,false>", "batch": B,
        "bytes_per_launch": fetch_b + write_b, "fetch_bytes_x2": fetch_b, "write_bytes": write_b,
        "raw_kib_per_dispatch": vals, "algorithmic_bytes": alg,
        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), tools/pmc_traffic.sh; FETCH doubled per the gfx950 correction"}

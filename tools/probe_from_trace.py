@@ -11,19 +11,21 @@ import csv
 import gzip
 import sys
 
-PROBES = [  # (kernel name as rocprof prints it, batch per launched block, GFLOP per image, label); the probe
-    # batch is the whole-tile batch bench.py picks at run time (_whole_tile_geo), read back from the grid
-    ("conv_gemm_kernel<96, 128, 1, 4, 1, true, false>", 128 / (64 * 64), 2.0 * 64 * 64 * 96 * 96 * 25 / 1e9,
-     "dominant: G13_5 modulated conv fwd 96->96 5x5 64x64"),
-    ("conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", 128 / (32 * 32), 2.0 * 32 * 32 * 128 * 128 * 9 / 1e9,
+PROBES = [  # (kernel name as rocprof prints it, threads per block, images per launched block, GFLOP per image,
+    # label); the probe batch is the one bench.py picks at run time (_whole_tile_geo), read back from the grid
+    ("conv_patch_x3_kernel<96, 12, 512, 5, 64, true, false>", 768, 1 / 8, 2.0 * 64 * 64 * 96 * 96 * 25 / 1e9,
+     "dominant: G13_5 modulated conv fwd 96->96 5x5 64x64 (split6 LDS-patch conv, 12 waves)"),
+    ("conv_patch_x3_kernel<96, 8, 512, 5, 64, true, false>", 512, 1 / 8, 2.0 * 64 * 64 * 96 * 96 * 25 / 1e9,
+     "dominant: G13_5 modulated conv fwd 96->96 5x5 64x64 (split6 LDS-patch conv, 8 waves)"),
+    ("conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", 256, 128 / (32 * 32), 2.0 * 32 * 32 * 128 * 128 * 9 / 1e9,
      "critic probe: D9_4 conv fwd 128->128 3x3 32x32"),
 ]
-PEAK = 157.3
+PEAK = 157.3 * 16 / 6      # the split6 pipe (bench.py SPLIT6_PIPE_PEAK_TFLOPS)
 
 path = sys.argv[1]
 rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-for kernel, per_block, gflop_img, label in PROBES:
+for kernel, threads, per_block, gflop_img, label in PROBES:
     best, run = [], []
     for r in rows:
         if kernel in r["Kernel_Name"] and (not run or r["Grid_Size_X"] == run[0]["Grid_Size_X"]):
@@ -41,11 +43,12 @@ for kernel, per_block, gflop_img, label in PROBES:
     if len(best) < 20:
         print(f"{label}: no run of >= 20 consecutive launches of {kernel}")
         continue
-    blocks = int(best[0]["Grid_Size_X"]) // 256
+    blocks = int(best[0]["Grid_Size_X"]) // threads
     B = round(blocks * per_block)
     gflop = gflop_img * B
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in best[3:]]
     avg = sum(d) / len(d)
     print(f"{label}: {kernel} at {blocks} blocks (B={B}), {len(d)} launches (run of {len(best)}, first 3 skipped)")
     print(f"  average {avg:.1f} us  min {min(d):.1f}  max {max(d):.1f}  -> {gflop / avg * 1e3:.1f} TF/s "
-          f"({gflop:.2f} GFLOP per launch), {gflop / avg * 1e3 / PEAK:.3f} of {PEAK}")
+          f"({gflop:.2f} GFLOP per launch), {gflop / avg * 1e3 / PEAK:.3f} of the split6 pipe {PEAK:.1f}, "
+          f"{gflop / avg * 1e3 / 157.3:.3f} of the fp32 MFMA peak 157.3")
