@@ -196,8 +196,10 @@ class Train(CheckpointMixin):
 
     def _penalty_stream(self):
         """The second stream of discriminator_backward (one per caller stream, so a captured graph and
-        an eager step never share it), or None off the GPU / for critics other than D9_4."""
-        if self.device.type != "cuda" or not isinstance(self.discriminator, Discriminator):
+        an eager step never share it), or None off the GPU / for critics other than D9_4 / with
+        ``penalty_overlap`` off (an A/B switch; bench.py --gp-overlap)."""
+        if (self.device.type != "cuda" or not isinstance(self.discriminator, Discriminator)
+                or not getattr(self, "penalty_overlap", True)):
             return None
         cur = torch.cuda.current_stream()
         streams = self.__dict__.setdefault("_gp_streams", {})
