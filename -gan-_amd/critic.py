@@ -516,7 +516,7 @@ class _PenaltyFn(Function):
 
 def penalty_sweeps(D, x_hat):
     """The part of the gradient penalty that depends on x_hat only: the forward and the input-gradient
-    sweep of D at x_hat (no autograd node; may run on a second stream, see wgangp.Train)."""
+    sweep of D at x_hat (no autograd node)."""
     run = Run(program_of(D), 1)
     x_hat = x_hat.detach().contiguous()
     run.forward(x_hat)
@@ -524,18 +524,9 @@ def penalty_sweeps(D, x_hat):
     return run, run.backward(seed, params=False, need_input=True)
 
 
-def adopt(run, g, stream):
-    """Tensors of ``penalty_sweeps`` made on another stream are used on ``stream`` from here on (the
-    caching allocator must not hand their memory out before that stream's use is done)."""
-    if torch.cuda.is_current_stream_capturing():      # a captured graph's pool frees nothing mid-replay
-        return
-    for t in [g, run.x] + [r for r in run.regions if r is not None]:
-        t.record_stream(stream)
-
-
 def penalty_value(D, run, g, center=1.0, lam=1.0, mode=0):
     """The fused penalty on the input gradient g of ``penalty_sweeps``; its ``.backward()`` runs the
-    double backward (tangent + adjoint sweeps) on the stream current at that call."""
+    double backward (tangent + adjoint sweeps)."""
     params = [p for p in program_of(D).params if p.requires_grad]
     if not params or not torch.is_grad_enabled():
         return _penalty(g, center, lam, mode)[0]

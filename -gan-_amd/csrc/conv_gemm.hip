@@ -17,10 +17,10 @@
 // nn.ConvTranspose2d (generator_13_5.py:156,594), and their autograd backward.
 //
 // Tiling.  256 threads = 4 waves; block tile BM x BN, K-step BK = 16; each wave owns a
-// (32*TM) x (32*TN) sub-tile of v_mfma_f32_32x32x2f32.  Both operand tiles sit in LDS
-// "k-contiguous" ([m][k], [n][k], row stride BK+2 floats) so that one lane reads its 8 k-values
-// of a row with four conflict-free ds_read_b64.  The MFMA k index is permuted: in step s lane
-// half h contributes k = 8h + s, identically for A and B, so the product is unchanged.
+// (MB*TM) x (MB*TN) sub-tile of MB x MB MFMA blocks.  fp32 products run as six bf16 products of
+// exactly split operands (split6, below): the conv fwd/dgrad body (conv_body_x3) stages the split
+// planes in LDS; the wgrad body keeps fp32 tiles in LDS ("k-contiguous" [m][k] / [n][k], row
+// stride BK+2 floats, four conflict-free ds_read_b64 per lane) and splits the fragments it reads.
 // Global gathers are branch-free (every lane loads from a valid address, padding is a select)
 // so hipcc keeps all of a tile's loads in flight; per-(channel,sample) scales are applied when
 // the prefetched registers are written to LDS.  Tiles are double buffered (one barrier per
@@ -282,7 +282,7 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 // lane's 8 k-values are rounded to bf16 (RNE) and ONE v_mfma_f32_32x32x16_bf16 replaces the 8
 // f32 steps -- its operand map is exactly this one (lane (r, h) holds A[r][8h + j] and
 // B[8h + j][r], j = 0..7) and its C/D map that of 32x32x2 f32, so nothing else changes.
-// ---- fp32 products on the bf16 matrix cores (GANAMD_SPLIT6) ----------------------------------
+// ---- fp32 products on the bf16 matrix cores (split6) --------------------------------------------
 // x = h + m + l with h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (RNE; the two differences
 // are exact in fp32), so x is kept to 24 significant bits.  x * y is then the six bf16 products
 // with at least one high part -- hh + (hm + mh) + (hl + lh + mm) -- exact in the MFMA; the three
@@ -290,9 +290,6 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ base, float 
 // v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) replace eight v_mfma_f32_32x32x2_f32 (8 x 64); 16-row
 // blocks: six half-rate v_mfma_f32_16x16x16_bf16 here, three paired full-rate 16x16x32 in the LDS
 // body (mfma_tile_x3).
-#ifndef GANAMD_SPLIT6
-#define GANAMD_SPLIT6 1
-#endif
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -358,28 +355,18 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
       b[j][0] = t0[0]; b[j][1] = t0[1]; b[j][2] = t1[0]; b[j][3] = t1[1];
     }
 
-    if constexpr (GANAMD_SPLIT6) {
-      // 16x16x16 bf16: lane (r, q) holds A[r][4q..4q+3] -- this map.  (Pairing the products on
-      // the full-rate 16x16x32 as mfma_tile_x3 does needs 8 k per lane: twice the fp32 LDS reads
-      // and splits here, measured 30 % slower on the 96-wide wgrad tiles.)
-      bf16x4 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
+    // 16x16x16 bf16: lane (r, q) holds A[r][4q..4q+3] -- this map.  (Pairing the products on the
+    // full-rate 16x16x32 as mfma_tile_x3 does needs 8 k per lane: twice the fp32 LDS reads and
+    // splits here, measured 30 % slower on the 96-wide wgrad tiles.)
+    bf16x4 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
 #pragma unroll
-      for (int i = 0; i < C::TM; ++i) split3<4>(a[i], ah[i], am[i], al[i]);
+    for (int i = 0; i < C::TM; ++i) split3<4>(a[i], ah[i], am[i], al[i]);
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j) split3<4>(b[j], bh[j], bm[j], bl[j]);
+    for (int j = 0; j < C::TN; ++j) split3<4>(b[j], bh[j], bm[j], bl[j]);
 #pragma unroll
-      for (int i = 0; i < C::TM; ++i)
+    for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-        for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_16(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
-      return;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_16(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
     return;
   } else {
   const int r = lane & 31, h = lane >> 5;
@@ -405,25 +392,15 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
     return;
   }
-  if constexpr (GANAMD_SPLIT6) {
-    bf16x8 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
+  bf16x8 ah[C::TM], am[C::TM], al[C::TM], bh[C::TN], bm[C::TN], bl[C::TN];
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i) split3<8>(a[i], ah[i], am[i], al[i]);
+  for (int i = 0; i < C::TM; ++i) split3<8>(a[i], ah[i], am[i], al[i]);
 #pragma unroll
-    for (int j = 0; j < C::TN; ++j) split3<8>(b[j], bh[j], bm[j], bl[j]);
+  for (int j = 0; j < C::TN; ++j) split3<8>(b[j], bh[j], bm[j], bl[j]);
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i)
+  for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_32(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
-    return;
-  }
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < C::TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = mfma6_32(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
   }
 }
 
@@ -831,12 +808,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const typename 
 #ifndef GANAMD_WGRAD_WPE
 #define GANAMD_WGRAD_WPE 1
 #endif
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
-__device__ __forceinline__ void conv_body_f32(const ConvArgs& p);
-
 
 // ---- fp32 GEMM body with split operands in LDS ----------------------------------------------
-// conv_body_f32's block schedule and gather, but each operand element is split ONCE -- by the
+// The conv block schedule (ConvPlan) and gather; each operand element is split ONCE -- by the
 // thread that stores it to LDS -- into three bf16 planes (h, m, l: split3); the waves read bf16
 // fragments and issue the six split products per 16 k on the bf16 matrix cores (mfma6_32 /
 // mfma6_16) instead of splitting every fragment they read.  K-step 16; 48-byte plane rows (16 k
@@ -1067,168 +1041,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GANAMD
 void conv_gemm_kernel(ConvArgs p) {
   if constexpr (BF16) {
     conv_body_bf16<BM, BN, WGM, WGN, MODE, BSCALE>(p);
-  } else if constexpr (GANAMD_SPLIT6) {
-    conv_body_x3<BM, BN, WGM, WGN, MODE, BSCALE>(p);
   } else {
-    conv_body_f32<BM, BN, WGM, WGN, MODE, BSCALE>(p);
+    conv_body_x3<BM, BN, WGM, WGN, MODE, BSCALE>(p);
   }
-}
-
-template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
-__device__ __forceinline__ void conv_body_f32(const ConvArgs& p) {
-  constexpr bool BF16 = false;
-  using C = TileCfg<BM, BN, WGM, WGN>;
-  constexpr int A4 = BM * BK / 4;                      // 16-byte slots of the A tile
-  constexpr int EA = (A4 + kThreads - 1) / kThreads;   // slots per thread
-  constexpr int KPT = BK * BN / kThreads;              // B k-values per thread
-  static_assert(KPT % 2 == 0 && BK % KPT == 0, "B mapping");
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int nct = p.Ckp / BK;
-  const int kt_total = nct * p.T;
-  int tx, ty, kt0, kt1, split = -1;
-  {
-    const int bid = blockIdx.x;
-    if (bid < p.full_blocks) {
-      ty = bid % p.gy;
-      tx = bid / p.gy;
-      kt0 = 0;
-      kt1 = kt_total;
-    } else {
-      const int t = bid - p.full_blocks;
-      const int r = t / p.S;
-      split = t - r * p.S;
-      ty = r % p.gy;
-      tx = p.nfull_t + r / p.gy;
-      kt0 = split * p.kt_per_split;
-      kt1 = min(kt_total, kt0 + p.kt_per_split);   // never empty: S = ceil(kt_total / kt_per_split)
-    }
-  }
-  const int n0 = tx * BN, m0 = ty * BM;
-
-  // A slots: row m = slot/SPR, k = 4*(slot%SPR) (+ kt*BK): contiguous along the packed row
-  constexpr int SPR = BK / 4;
-  const int Krow = p.T * p.Ckp;
-  const rsrc_t rw = make_rsrc(p.w, p.w_bytes);
-  int a_off[EA];
-#pragma unroll
-  for (int e = 0; e < EA; ++e) {
-    const int slot = tid + e * kThreads;
-    a_off[e] = 4 * ((m0 + slot / SPR) * Krow + 4 * (slot % SPR));
-  }
-
-  // B: pixel n = n0 + tid % BN, channels c0 + kg*KPT .. +KPT-1 of the K-step
-  const int b_n = tid % BN, b_kg = tid / BN;
-  const Gather& g = p.g;
-  const int gn = n0 + b_n;
-  const bool n_ok = gn < p.N;
-  int bb = 0, oh = 0, ow = 0;
-  if (n_ok) {
-    bb = gn / p.ohw;
-    const int rr = gn - bb * p.ohw;
-    if (MODE == kTransposed && p.om.s == -2) {
-      ring_coord(rr, p.om.qh, p.om.qw, p.om.OW, p.om.OWp, oh, ow);
-    } else {
-      oh = rr / g.OW;
-      ow = rr - oh * g.OW;
-    }
-  }
-  const unsigned cs4 = 4u * (unsigned)(g.B * g.H * g.W);
-  const int img = bb * g.H * g.W;
-  const rsrc_t rx = make_rsrc(g.src, g.src_bytes());
-  const rsrc_t rsc = make_rsrc(BSCALE ? g.scale : g.src, BSCALE ? g.scale_bytes() : 0);
-
-  // one K-step's operands in flight: the A slots and the B gather (+ its per-(channel, sample) scales)
-  struct Stage {
-    f32x4 ra[EA];
-    float rb[KPT], rs[KPT];
-  };
-  // (cc, kh, kw): channel chunk and tap of the next K-step to load (k = (cc, t, c16))
-  int cc = kt0 / p.T;
-  int kh, kw;
-  {
-    const int t = kt0 - cc * p.T;
-    kh = t / g.KW;
-    kw = t - kh * g.KW;
-  }
-  auto tap = [&]() { return n_ok ? tap_offset<MODE>(g, oh, ow, kh, kw) : -1; };
-  int sp = tap();
-
-  auto gload = [&](int kt, Stage& S) {
-#pragma unroll
-    for (int e = 0; e < EA; ++e)
-      if (tid + e * kThreads < A4) S.ra[e] = bload4(rw, a_off[e] + kt * (BK * 4));
-    const int c = cc * BK + b_kg * KPT;
-    // channels past the source's end fall outside the buffer: the hardware returns 0
-    const unsigned base = sp >= 0 ? 4u * (unsigned)(img + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
-    const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + bb) : (unsigned)kOOB;
-#pragma unroll
-    for (int e = 0; e < KPT; ++e) {
-      S.rb[e] = bload(rx, (int)(base + (unsigned)e * cs4));
-      if (BSCALE) S.rs[e] = bload(rsc, (int)(sbase + 4u * (unsigned)(e * g.B)));
-    }
-    if (++kw == g.KW) {
-      kw = 0;
-      if (++kh * g.KW >= p.T) {
-        kh = 0;
-        ++cc;
-      }
-    }
-    sp = tap();
-  };
-  auto sstore = [&](int buf, const Stage& S) {
-    const f32x4* ra = S.ra;
-    const float* rb = S.rb;
-    const float* rs = S.rs;
-#pragma unroll
-    for (int e = 0; e < EA; ++e) {
-      const int slot = tid + e * kThreads;
-      if (slot < A4) {
-        float* d = &As[buf][(slot / SPR) * LDK + 4 * (slot % SPR)];
-        *reinterpret_cast<f32x2*>(d) = f32x2{ra[e][0], ra[e][1]};
-        *reinterpret_cast<f32x2*>(d + 2) = f32x2{ra[e][2], ra[e][3]};
-      }
-    }
-    float* d = &Bs[buf][b_n * LDK + b_kg * KPT];
-#pragma unroll
-    for (int e = 0; e < KPT; e += 2)
-      *reinterpret_cast<f32x2*>(d + e) =
-          BSCALE ? f32x2{rb[e] * rs[e], rb[e + 1] * rs[e + 1]} : f32x2{rb[e], rb[e + 1]};
-  };
-
-  typename C::acc_t acc[C::TM][C::TN];
-  zero_acc<C>(acc);
-
-  Stage s0;
-  // two K-steps in flight: the gather for step kt+2 is issued while step kt's MFMAs run and step
-  // kt+1's operands (loaded one step earlier) go to LDS -- twice the latency cover per wave
-  Stage s1;
-  gload(kt0, s0);
-  sstore(0, s0);
-  if (kt0 + 1 < kt1) gload(kt0 + 1, s1);
-  __syncthreads();
-  int kt = kt0;
-  for (; kt + 1 < kt1; kt += 2) {
-    if (kt + 2 < kt1) gload(kt + 2, s0);
-#pragma unroll
-    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[0], Bs[0], acc, lane, wm, wn, k0);
-    sstore(1, s1);
-    __syncthreads();
-    if (kt + 3 < kt1) gload(kt + 3, s1);
-#pragma unroll
-    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[1], Bs[1], acc, lane, wm, wn, k0);
-    if (kt + 2 < kt1) sstore(0, s0);
-    __syncthreads();
-  }
-  if (kt < kt1) {
-#pragma unroll
-    for (int k0 = 0; k0 < BK; k0 += 16) mfma_tile<C, LDK, BF16>(As[0], Bs[0], acc, lane, wm, wn, k0);
-  }
-
-  conv_epilogue<C, MODE>(p, acc, n0, m0, split, lane, wm, wn);
 }
 
 // Batched repack: block b finds its job by binary search over the jobs' chunk offsets and packs

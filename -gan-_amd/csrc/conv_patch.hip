@@ -116,7 +116,12 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   const int wrow = (wv % WM) * TM * MB, wcol = (wv / WM) * PW;   // this wave's rows / pixels
   const int H = p.H, HW = H * TW;
   const int gy = (p.M + BM - 1) / BM;
-  const int ty = blockIdx.x % gy, reg = blockIdx.x / gy;
+  // XCD-aware order: blocks b and b + 8 land on one XCD (round-robin dispatch), so block b takes
+  // tile (b % 8) * (nb / 8) + b / 8 -- each XCD runs a contiguous range of row tiles and adjacent
+  // tiles' halo rows are fetched from HBM once into that XCD's L2 (PMC: 1.33x -> see DESIGN §3)
+  int bid = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bid = (bid & 7) * (int)(gridDim.x >> 3) + (bid >> 3);
+  const int ty = bid % gy, reg = bid / gy;
   const int tiles_img = H / TH;
   const int b = reg / tiles_img, oh0 = (reg - b * tiles_img) * TH;
   const int m0 = ty * BM;

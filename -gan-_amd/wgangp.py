@@ -169,44 +169,10 @@ class Train(CheckpointMixin):
         pred_r, pred_f = pred[:b_size], pred[b_size:]
         real_loss = -torch.mean(pred_r)
         fake_loss = torch.mean(pred_f)
-        # The penalty's forward and input-gradient sweep (wgangp.py:34-54) depend on the two batches
-        # only: they run on a second HIP stream concurrently with the first-order backward -- the
-        # critic's small-map layers leave most of the chip idle, two sweeps fill it.  The fork comes
-        # after the first-order forward has been issued (its plan set-up packs every weight copy the
-        # penalty's sweeps read); the penalty value, its autograd node and its double backward
-        # (tangent + adjoint sweeps) are made on this stream after the join, so the weight gradients
-        # accumulate in the reference's order and no autograd node lives on the second stream.
-        side = self._penalty_stream()
-        if side is None:
-            (real_loss + fake_loss).backward()
-            gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
-        else:
-            cur = torch.cuda.current_stream()
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                eps = self.rng.rand((b_size,)).view(b_size, 1, 1, 1)
-                x_interp = ((1 - eps) * images + eps * gen_imgs.detach()).detach()
-                run, g = critic.penalty_sweeps(self.discriminator, x_interp)
-            (real_loss + fake_loss).backward()
-            cur.wait_stream(side)
-            critic.adopt(run, g, cur)
-            gp = 10 * critic.penalty_value(self.discriminator, run, g, 1.0, 1.0, 0)
+        (real_loss + fake_loss).backward()
+        gp = 10 * self.gradient_penalty(images, gen_imgs, b_size, self.device)
         gp.backward()
         return real_loss, fake_loss, gp
-
-    def _penalty_stream(self):
-        """The second stream of discriminator_backward (one per caller stream, so a captured graph and
-        an eager step never share it), or None off the GPU / for critics other than D9_4 / with
-        ``penalty_overlap`` off (an A/B switch; bench.py --gp-overlap)."""
-        if (self.device.type != "cuda" or not isinstance(self.discriminator, Discriminator)
-                or not getattr(self, "penalty_overlap", True)):
-            return None
-        cur = torch.cuda.current_stream()
-        streams = self.__dict__.setdefault("_gp_streams", {})
-        s = streams.get(cur.cuda_stream)
-        if s is None:
-            s = streams[cur.cuda_stream] = torch.cuda.Stream(device=self.device)
-        return s
 
     def train(self, checkpoints=True):
         """Epoch loop of train/wgangp.py:73-95: resume from ``checkpoint/.pth`` if present, one

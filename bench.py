@@ -71,9 +71,6 @@ def parse():
     ap.add_argument("--patch", choices=["on", "off"], default="on",
                     help="stride-1 convs on 32/64-wide maps through the split6 LDS-patch conv and the row-blocked "
                          "weight gradient (default) or the gather GEMMs (ganamd_conv_set_patch 7 / 0; A/B)")
-    ap.add_argument("--gp-overlap", choices=["on", "off"], default="on",
-                    help="the penalty's forward + input-gradient sweeps on a second stream during the first-order "
-                         "backward (default) or after it on the same stream (A/B)")
     ap.add_argument("--fake-groups", default=None, metavar="K,K,...",
                     help="fake-batch groups of the n_critic steps, each one generator forward with segmented "
                          "BatchNorm (default: the headline schedule FAKE_GROUPS)")
@@ -394,7 +391,6 @@ def build(args, dev, rank, world):
                                         precision=args.precision)
     else:
         tr = gan_amd.Train([], dev, 1, 256, G, args.config, D, args.config, rng=rng)
-        tr.penalty_overlap = args.gp_overlap == "on"
     B = args.batch
     if args.config != "lazy":
         return G, D, tr, Iteration(tr, B, N_CRITIC, world, *fake_schedule(args, B, world))
@@ -588,8 +584,7 @@ def main():
             "dtype": "fp32" if args.precision == "fp32" else "bf16 GEMM operands, fp32 accumulate/storage; fp32 R1/R2/GP steps",
             "data": "synthetic N(0,1) real batches drawn on device each critic step; random reference-init weights",
             "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
-                       "parallelism": f"dp{world}", "mode": args.mode, "patch_conv": args.patch,
-                       "gp_overlap": args.gp_overlap},
+                       "parallelism": f"dp{world}", "mode": args.mode, "patch_conv": args.patch},
         }
         if headline:
             out["config"]["n_critic"] = N_CRITIC
