@@ -46,6 +46,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kOOB = (int)0x80000000;
+constexpr int kMaxScale = 1024;   // input channels whose scales the block stages in LDS
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
@@ -111,6 +112,10 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int kStoreTap = T > 4 ? 3 : T - 1;
   static_assert(TN >= 1 && TM * MB * WM == BM && TN * MB == PW && WM * WN == NW, "tile");
   __shared__ __attribute__((aligned(16))) unsigned short Ps[2 * BUF];
+  // the block's modulation scales s[c][b] (one image per block: one value per input channel),
+  // staged once so the patch stores read them from LDS -- a global load there would make every
+  // store wait for all of the wave's loads in flight (vmcnt is in order)
+  __shared__ __attribute__((aligned(16))) float Ssc[BSCALE ? kMaxScale : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wrow = (wv % WM) * TM * MB, wcol = (wv / WM) * PW;   // this wave's rows / pixels
@@ -163,8 +168,9 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
       const int cg = u / NPOS, pos = u - cg * NPOS;
       f32x4 v = pv[e];
       if constexpr (BSCALE) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(&Ssc[cc * 16 + 4 * cg]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] *= bload(rsc, 4 * ((cc * 16 + 4 * cg + q) * p.B + b));
+        for (int q = 0; q < 4; ++q) v[q] *= sc[q];
       }
       bf16x4 h, m, l;
       split4(v, h, m, l);
@@ -245,12 +251,16 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
       }
   };
 
-  // prologue: chunk 0's patch and tap 0's A fragments
+  // prologue: the block's scales, chunk 0's patch and tap 0's A fragments
   bf16x8 fa[2][TM][3];
   {
     f32x4 pv[UPT];
     patch_load(0, pv);
     a_load(DGRAD ? T - 1 : 0, fa[0]);
+    if constexpr (BSCALE) {
+      for (int c = tid; c < p.Ckp; c += NT) Ssc[c] = bload(rsc, 4 * (c * p.B + b));   // Ckp <= kMaxScale (launch)
+      __syncthreads();
+    }
     patch_store(Ps, 0, pv);
   }
   __syncthreads();
@@ -266,14 +276,17 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
         const int tt = t + u;
         if (tt < T) {
           const int kt = cc * T + tt;
+          bf16x8 fb[TN][3];
+          b_read(P, kh * PWD + kw, fb);
+          mfma(fa[u], fb);
+          // loads AFTER the products are issued: the wait for this tap's weights (above) then
+          // never covers the loads of the next tap or chunk (vmcnt counts in order), and they
+          // overlap the products all the same
           if (kt + 1 < nct * T) {                               // the next tap's weights
             const int nt = (tt + 1 == T) ? 0 : tt + 1, nc = (tt + 1 == T) ? cc + 1 : cc;
             a_load(nc * T + (DGRAD ? T - 1 - nt : nt), fa[u ^ 1]);
           }
           if (tt == 0 && more) patch_load(cc + 1, pv);          // the next chunk's patch
-          bf16x8 fb[TN][3];
-          b_read(P, kh * PWD + kw, fb);
-          mfma(fa[u], fb);
           // the idle buffer (last read in chunk cc - 1), a few taps after its loads were issued
           if (tt == kStoreTap && more) patch_store(Ps + ((cc + 1) & 1) * BUF, cc + 1, pv);
           if (++kw == KK) {
@@ -292,8 +305,8 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
     };
     // the tap loop: fully unrolled where the registers allow it (48-row blocks, the 4-wave W = 32
     // blocks: the taps' index math, weight prefetch and patch stores resolve at compile time and the
-    // next tap's fragment reads can be scheduled under the current tap's products); the 8-wave 96-row
-    // blocks spill when unrolled and keep a loop of two taps
+    // next tap's fragment reads can be scheduled under the current tap's products); the 12-wave 96-row
+    // blocks spill when unrolled (or with the first taps peeled) and keep a loop of two taps
     if constexpr (BM == 48 || NW == 4) {
 #pragma unroll
       for (int t = 0; t < T; t += 2) tap_pair(t);
@@ -395,7 +408,9 @@ int occupancy(const Args& a) {
 }
 
 hipError_t launch(const Args& a, hipStream_t st) {
-  if (!domain(a.M, a.H, a.W, a.KK, 1, (a.KK - 1) / 2, a.H, a.W) || !a.w || !a.src || !a.y) return hipErrorInvalidValue;
+  if (!domain(a.M, a.H, a.W, a.KK, 1, (a.KK - 1) / 2, a.H, a.W) || !a.w || !a.src || !a.y ||
+      (a.scale && a.Ckp > kMaxScale))
+    return hipErrorInvalidValue;
   return dispatch(a, st, false, nullptr);
 }
 
