@@ -693,11 +693,11 @@ __device__ __forceinline__ void conv_body_bf16(const ConvArgs& p) {
   __syncthreads();
   int kt = kt0;
   for (; kt + 1 < kt1; kt += 2) {
-    if (kt + 2 < kt1) gload(kt + 2, s0);
+    gload(kt + 2, s0);              // unconditional (past the range: zeros), see conv_body_x3
     mfma_step(0);
     sstore(1, s1);
     __syncthreads();
-    if (kt + 3 < kt1) gload(kt + 3, s1);
+    gload(kt + 3, s1);
     mfma_step(1);
     if (kt + 2 < kt1) sstore(0, s0);
     __syncthreads();
@@ -932,7 +932,7 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
   int a_off[EA];
 #pragma unroll
   for (int e = 0; e < EA; ++e) {
-    const int slot = tid + e * kThreads;
+    const int slot = min(tid + e * kThreads, SA - 1);
     a_off[e] = 4 * ((m0 + slot / SPR) * Krow + 8 * (slot % SPR));
   }
 
@@ -970,13 +970,17 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
   auto tap = [&]() { return n_ok ? tap_offset<MODE>(g, oh, ow, kh, kw) : -1; };
   int sp = tap();
 
+  // Every load is unconditional (a slot past the tile re-reads a valid one, a K-step past the
+  // range reads zeros or ignored rows within the buffer bounds): the compiler then knows how many
+  // loads are in flight and the wait for step kt+1's operands leaves step kt+2's gather in flight
+  // (after a conditional load it drains them all -- vmcnt counts in order).
   auto gload = [&](int kt, Stage& S) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e)
-      if (tid + e * kThreads < SA) {
-        S.ra[e][0] = bload4(rw, a_off[e] + kt * (BK * 4));
-        S.ra[e][1] = bload4(rw, a_off[e] + kt * (BK * 4) + 16);
-      }
+    for (int e = 0; e < EA; ++e) {
+      const int o = a_off[e] + kt * (BK * 4);
+      S.ra[e][0] = bload4(rw, o);
+      S.ra[e][1] = bload4(rw, o + 16);
+    }
     const int c = cc * BK + b_kg * KPT;
     const unsigned base = sp >= 0 ? 4u * (unsigned)(img + sp) + (unsigned)c * cs4 : (unsigned)kOOB;
     const unsigned sbase = sp >= 0 ? 4u * (unsigned)(c * g.B + bb) : (unsigned)kOOB;
@@ -1023,11 +1027,11 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
   __syncthreads();
   int kt = kt0;
   for (; kt + 1 < kt1; kt += 2) {
-    if (kt + 2 < kt1) gload(kt + 2, s0);
+    gload(kt + 2, s0);
     mfma_tile_x3<C, PSA, PSB>(As[0], Bs[0], acc, lane, wm, wn);
     sstore(1, s1);
     __syncthreads();
-    if (kt + 3 < kt1) gload(kt + 3, s1);
+    gload(kt + 3, s1);
     mfma_tile_x3<C, PSA, PSB>(As[1], Bs[1], acc, lane, wm, wn);
     if (kt + 2 < kt1) sstore(0, s0);
     __syncthreads();
