@@ -210,14 +210,12 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
     posb[j] = (q / TW) * PWD + q % TW;
   }
   const int bq0 = 0, bq1 = MB == 32 ? 1 : (fhi ? 0 : 1), bq2 = MB == 32 ? 2 : (fhi ? 2 : 1);
-  auto b_read = [&](const unsigned short* P, int toff, bf16x8 (&fb)[TN][3]) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int o = poff<MB>(posb[j] + toff, fhalf);
-      fb[j][0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
-      fb[j][1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
-      fb[j][2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
-    }
+  // the three B fragments of column block j at tap offset toff
+  auto b_frag = [&](const unsigned short* P, int toff, int j, bf16x8 (&f)[3]) {
+    const int o = poff<MB>(posb[j] + toff, fhalf);
+    f[0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
+    f[1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
+    f[2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
   };
 
   acc_t acc[TM][TN];
@@ -228,27 +226,26 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 
-  auto mfma = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TN][3]) {
+  // the products of column block j (B fragments fb) with all of the wave's row blocks
+  auto mfma_j = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[3], int j) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (MB == 32) {
+        // l*h, h*l, m*m, m*h, h*m, h*h: smallest first into the same accumulator
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i][j], 0, 0, 0);
+      } else {
+        // (h|m)x(h|h) = hh + mh, (h|l)x(m|h) = hm + lh, (m|h)x(m|l) = mm + hl: lanes q < 2 carry
+        // the first 16-k half of the 32, q >= 2 the second (the same 16 channels)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (MB == 32) {
-          // l*h, h*l, m*m, m*h, h*m, h*h: smallest first into the same accumulator
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-        } else {
-          // (h|m)x(h|h) = hh + mh, (h|l)x(m|h) = hm + lh, (m|h)x(m|l) = mm + hl: lanes q < 2 carry
-          // the first 16-k half of the 32, q >= 2 the second (the same 16 channels)
-#pragma unroll
-          for (int t = 0; t < 3; ++t)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][t], fb[j][t], acc[i][j], 0, 0, 0);
-        }
+        for (int t = 0; t < 3; ++t)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][t], fb[t], acc[i][j], 0, 0, 0);
       }
+    }
   };
 
   // prologue: the block's scales, chunk 0's patch and tap 0's A fragments
@@ -269,6 +266,12 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
     const bool more = cc + 1 < nct;
     f32x4 pv[UPT];
     int kh = 0, kw = 0;
+    // B fragments rotate one column block ahead: block j + 1's (or the next tap's block 0) reads are
+    // issued before block j's products, so each read has a block of products to arrive under instead
+    // of exposing its latency right before the product that needs it.  After the chunk's last tap
+    // the look-ahead re-reads position 0 (a dummy: the next chunk's patch is behind the barrier).
+    bf16x8 cur[3];
+    b_frag(P, 0, 0, cur);
     auto tap_pair = [&](int t) {
       // two taps per iteration: register double buffer fa[0] / fa[1] without dynamic indexing
 #pragma unroll
@@ -276,9 +279,20 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
         const int tt = t + u;
         if (tt < T) {
           const int kt = cc * T + tt;
-          bf16x8 fb[TN][3];
-          b_read(P, kh * PWD + kw, fb);
-          mfma(fa[u], fb);
+          const int toff = kh * PWD + kw;
+          const int tnext = tt + 1 == T ? -posb[0] : (kw + 1 == KK ? toff + PWD - (KK - 1) : toff + 1);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            bf16x8 nxt[3];
+            if (j + 1 < TN)
+              b_frag(P, toff, j + 1, nxt);
+            else
+              b_frag(P, tnext, 0, nxt);
+            __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead of the products
+            mfma_j(fa[u], cur, j);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) cur[q] = nxt[q];
+          }
           // loads AFTER the products are issued: the wait for this tap's weights (above) then
           // never covers the loads of the next tap or chunk (vmcnt counts in order), and they
           // overlap the products all the same
