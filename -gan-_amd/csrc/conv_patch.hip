@@ -97,15 +97,11 @@ __device__ __forceinline__ int mfma_row(int lane, int r) {
 template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
 __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int NT = 64 * NW;
-  // waves along M: 8-wave 96-row blocks split the rows two ways (48 rows x 128 pixels per wave: half
-  // the weight fragments per wave, 2 waves per SIMD); otherwise every wave owns all rows
-  constexpr int WM = (BM == 96 && NW == 8) ? 2 : 1, WN = NW / WM;
+  // waves along M: 12-wave 96-row blocks split the rows three ways (32 rows x 128 pixels per wave: a
+  // third of the weight fragments per wave, 3 waves per SIMD); otherwise every wave owns all rows
+  constexpr int WM = (BM == 96 && NW == 12) ? 3 : 1, WN = NW / WM;
   constexpr int PW = NPIX / WN;                             // pixels per wave
-  // MFMA block edge: 16 (v_mfma_f32_16x16x32_bf16 on paired split products) wherever the rows allow
-  // -- on random operands it sustains 347 split6 TF/s at any waves/SIMD where the 32x32x16 form
-  // holds 202-236 at 2-4 waves/SIMD (tools/mfma_peak_bf16.hip, profiles/r04_mfma_ceiling_bf16.txt)
-  constexpr int MB = (BM % 32 == 0 && NW == 4) ? 32 : 16;
-  static_assert(MB == 16 || WM == 1, "row split");
+  constexpr int MB = (BM % 32 == 0) ? 32 : 16;              // MFMA block edge (48 rows: 16)
   constexpr int TM = BM / (MB * WM), TN = PW / MB, NR = MB == 32 ? 16 : 4;
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
   constexpr int TH = NPIX / TW, PAD = (KK - 1) / 2, T = KK * KK;
@@ -374,7 +370,7 @@ int occ_of() {
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
   if (a.W == 64) {
-    constexpr int NW = 8;
+    constexpr int NW = BM == 96 ? 12 : 8;
     if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
       hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),

@@ -337,15 +337,12 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   }
 }
 
-// tile of M rows: 16-row blocks (paired 16x16x32) x 3 waves for M <= 48, else 32-row blocks, one wave
-// each; 3x3 convs with M <= 64 take two 32-column blocks per wave (each A fragment feeds twice the
-// products: the staging per product that bounds the narrow tile drops by a third)
+// tile of M rows: 16-row blocks (paired 16x16x32) x 3 waves for M <= 48, else 32-row blocks, one wave each
 struct Tile {
   int mb, nw, tn;
 };
-Tile tile_of(int M, int K) {
+Tile tile_of(int M) {
   if (M <= 48) return {16, 3, 3};
-  if (M <= 64 && K == 3) return {32, 2, 2};
   return {32, (M + 31) / 32, 1};
 }
 
@@ -358,12 +355,8 @@ hipError_t go(const Args& a, hipStream_t st) {
 
 template <int KK, bool S>
 hipError_t go_tile(const Args& a, hipStream_t st) {
-  const Tile t = tile_of(a.M, KK);
+  const Tile t = tile_of(a.M);
   if (t.mb == 16) return go<16, 3, 3, KK, S>(a, st);
-  if (t.tn == 2) {
-    if constexpr (KK == 3) return go<32, 2, 2, KK, S>(a, st);
-    return hipErrorInvalidValue;
-  }
   switch (t.nw) {
     case 2: return go<32, 2, 1, KK, S>(a, st);
     case 3: return go<32, 3, 1, KK, S>(a, st);
@@ -382,7 +375,7 @@ bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW, int
 // Split-K: enough blocks for about two rounds of the chip at the kernel's occupancy (~2 blocks per
 // CU), each split at least 16 K-steps (512 pixels).
 void plan(int M, int J, int B, int H, int W, int K, int segs, int cus, int* splits, int* ks_per_split) {
-  const Tile t = tile_of(M, K);
+  const Tile t = tile_of(M);
   const long tiles = (long)((J + t.tn * t.mb - 1) / (t.tn * t.mb)) * ((M + t.nw * t.mb - 1) / (t.nw * t.mb)) * K;
   const long ks_total = (long)segs * B * H * W / KS;
   const long target = 4L * cus;
