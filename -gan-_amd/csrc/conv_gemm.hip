@@ -258,20 +258,6 @@ struct TileCfg {
   static_assert(WGM * WGN == 4, "4 waves per block");
   static_assert(TM * MB * WGM == BM && TN * MB * WGN == BN, "tile must split into MFMA blocks");
 };
-// The split6 LDS body's tiles: GANAMD_X3_MB (32: 32x32 blocks where the wave tile allows, six
-// v_mfma_f32_32x32x16_bf16 per 16 k; 16: 16x16 blocks, three paired v_mfma_f32_16x16x32_bf16)
-#ifndef GANAMD_X3_MB
-#define GANAMD_X3_MB 32
-#endif
-template <int BM, int BN, int WGM, int WGN>
-struct TileCfgX3 {
-  static constexpr int MB = (GANAMD_X3_MB == 16 && BN <= 128) ? 16 : TileCfg<BM, BN, WGM, WGN>::MB;
-  static constexpr int TM = BM / (MB * WGM);
-  static constexpr int TN = BN / (MB * WGN);
-  static constexpr int NR = MB == 32 ? 16 : 4;
-  using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
-  static_assert(TM * MB * WGM == BM && TN * MB * WGN == BN, "tile must split into MFMA blocks");
-};
 // C/D map of the block MFMAs: lane's register r holds row mfma_row<MB>(lane, r), column lane % MB
 template <int MB>
 __device__ __forceinline__ int mfma_row(int lane, int r) {
@@ -907,7 +893,7 @@ __device__ __forceinline__ void store_split8(unsigned short* d, const float* v) 
 
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE>
 __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
-  using C = TileCfgX3<BM, BN, WGM, WGN>;
+  using C = TileCfg<BM, BN, WGM, WGN>;
   constexpr int SPR = BK / 8;                          // 8-k A slots per row and K-step
   constexpr int SA = BM * SPR;
   constexpr int EA = (SA + kThreads - 1) / kThreads;   // slots per thread
