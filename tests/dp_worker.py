@@ -136,6 +136,8 @@ def main_progan(out):
     dist.init_process_group("gloo")
     import gan_amd
     from gan_amd.pipeline import Iteration, restore, snapshot
+    if os.environ.get("GANAMD_TEST_PATCH_MASK"):      # diagnosis: kernel selection A/B
+        gan_amd.ops.LIB.ganamd_conv_set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
     dev = torch.device("cuda", 0)
     G, D = make_progan(gan_amd, dev)
     tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, progan_seed(rank)))

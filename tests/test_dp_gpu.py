@@ -204,6 +204,8 @@ def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
     assert got["world"] == W
 
     import gan_amd
+    if os.environ.get("GANAMD_TEST_PATCH_MASK"):      # diagnosis: kernel selection A/B (dp_worker too)
+        gan_amd.ops.LIB.ganamd_conv_set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
     dev = torch.device("cuda", 0)
     B = dp_worker.B_PROGAN
     G, D = dp_worker.make_progan(gan_amd, dev)

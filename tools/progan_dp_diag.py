@@ -15,8 +15,24 @@ def rel(a, b):
     return float((a - b).double().norm() / max(b.double().norm(), 1e-30))
 
 
+def poison():
+    """Fill the caching allocator's free blocks with NaN: a kernel that reads workspace it did not
+    write then shows up as NaN or a mismatch instead of reading the same leftovers every run."""
+    free = torch.cuda.mem_get_info()[0]
+    blocks = []
+    try:
+        for _ in range(64):
+            blocks.append(torch.full((1 << 28,), float("nan"), device="cuda"))   # 1 GiB each
+            if torch.cuda.mem_get_info()[0] < free // 4:
+                break
+    finally:
+        del blocks
+    torch.cuda.synchronize()
+
+
 def main():
     overlap = (sys.argv[1] != "0") if len(sys.argv) > 1 else True
+    do_poison = len(sys.argv) > 2 and sys.argv[2] == "poison"
     import gan_amd
     from gan_amd.pipeline import Iteration, restore, snapshot
     dev = torch.device("cuda", 0)
@@ -39,14 +55,20 @@ def main():
     it.step()
     replay = grab()
     restore(tr, snap)
+    if do_poison:
+        poison()
     it.eager()
     eager = grab()
     restore(tr, snap)
+    if do_poison:
+        poison()
     _shard_mean_iteration_1(tr, rng, B)
     loop = grab()
+    for k, v in loop.items():
+        print(f"[diag] non-finite in {k}: {int((~torch.isfinite(v)).sum())}", flush=True)
     for name, (x, y) in {"replay vs eager": (replay, eager), "eager vs shard loop": (eager, loop),
                          "replay vs shard loop": (replay, loop)}.items():
-        print(f"[diag] overlap={int(overlap)} {name}: " + "  ".join(f"{k} {rel(x[k], y[k]):.3e}" for k in x), flush=True)
+        print(f"[diag] overlap={int(overlap)} poison={int(do_poison)} {name}: " + "  ".join(f"{k} {rel(x[k], y[k]):.3e}" for k in x), flush=True)
 
 
 def _shard_mean_iteration_1(tr, rng, B):
