@@ -110,7 +110,7 @@ def main_graph(out):
 
 
 B_PROGAN = 64
-PROGAN_WORLD = 4
+PROGAN_WORLD = int(os.environ.get("GANAMD_TEST_PROGAN_WORLD", "4"))
 
 
 def progan_seed(rank):
@@ -141,7 +141,8 @@ def main_progan(out):
     dev = torch.device("cuda", 0)
     G, D = make_progan(gan_amd, dev)
     tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, progan_seed(rank)))
-    it = Iteration(tr, B_PROGAN, 5, world, overlap=True)       # bench.py's progan schedule (fake_schedule)
+    overlap = os.environ.get("GANAMD_TEST_PROGAN_OVERLAP", "1") != "0"     # diagnosis override
+    it = Iteration(tr, B_PROGAN, 5, world, overlap=overlap)    # bench.py's progan schedule (fake_schedule)
     snap = snapshot(tr)
     it.eager()
     it.capture()
