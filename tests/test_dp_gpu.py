@@ -16,7 +16,10 @@ two shards one after another and their gradients averaged by hand before every o
 
 test_dp_progan_four_ranks_match_shard_mean: config 5's split (the progan pair on 4 ranks, 64 images
 each, BASELINE.json) through the bench's progan schedule (fake batch of the next critic step on a
-side stream) against the four shards run one after another with hand-averaged gradients.
+side stream) against the four shards run one after another with hand-averaged gradients -- within
+3x of how far that shard mean moves when its four shards are summed in the opposite order (gloo's
+ring sums four buffers in its own order, and the iteration amplifies last-bit differences; with
+GANAMD_TEST_PROGAN_WORLD=2 the bar is the 1e-5 of the two-rank tests, measured passing).
 
 test_bench_two_ranks: ``bench.py --gpus 2 --backend gloo`` starts its own ranks and reports
 n_gpus 2 (it used to run one rank silently), in eager and in graph mode.
@@ -147,9 +150,10 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
     assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
 
 
-def _shard_mean_iteration(tr, rngs, B, groups):
+def _shard_mean_iteration(tr, rngs, B, groups, reverse=False):
     """One WGAN-GP iteration with the shards run one after another on the same weights and the
-    gradients of every optimizer step averaged by hand (gloo: SUM, then * 1/N)."""
+    gradients of every optimizer step averaged by hand (gloo: SUM, then * 1/N; ``reverse``: the
+    shards summed in the opposite order -- another legitimate fp32 rounding of the same mean)."""
     n = len(rngs)
     for k in set(groups):
         tr.generate_fakes(k, B)    # warm-up: the workers' warm-up recorded the noise shapes
@@ -159,6 +163,7 @@ def _shard_mean_iteration(tr, rngs, B, groups):
         fakes.append([f for k in groups for f in tr.generate_fakes(k, B)])
 
     def mean_into(flat_grad, gs):
+        gs = gs[::-1] if reverse else gs
         acc = gs[0].clone()
         for g in gs[1:]:
             acc.add_(g)
@@ -208,15 +213,36 @@ def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
         gan_amd.ops.LIB.ganamd_conv_set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
     dev = torch.device("cuda", 0)
     B = dp_worker.B_PROGAN
-    G, D = dp_worker.make_progan(gan_amd, dev)
-    tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, 1))
-    g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
-    rngs = [gan_amd.DeviceRNG(dev, dp_worker.progan_seed(r)) for r in range(W)]
-    _shard_mean_iteration(tr, rngs, B, [1] * 5)
+
+    def shard_mean(reverse):
+        G, D = dp_worker.make_progan(gan_amd, dev)
+        tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, 1))
+        g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
+        rngs = [gan_amd.DeviceRNG(dev, dp_worker.progan_seed(r)) for r in range(W)]
+        _shard_mean_iteration(tr, rngs, B, [1] * 5, reverse=reverse)
+        return tr, g0, d0
+
+    tr, g0, d0 = shard_mean(False)
     errs = _dp_errors(got, tr, g0, d0)
     print(f"progan {W}-rank DP vs shard mean:", errs)
-    assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
-    assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
+    if W <= 2:
+        # two shards sum the same way in any order (fp32 addition commutes): bit-level agreement
+        assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
+        assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
+        return
+    # With four shards gloo's ring sums them in another order than the hand-made mean, and this
+    # iteration amplifies a last-bit difference of the critic gradients (one shared PReLU slope per
+    # layer, five AdamW steps whose first update is ~lr * sign(g)) to ~1e-3 of the generator gradient.
+    # The bar is that spread itself: the same shard mean with the shards summed in reverse order.
+    mid = {k: v.detach().cpu().clone() for k, v in (("g_data", tr.optimizer_G.flat.data),
+                                                   ("g_grad", tr.optimizer_G.flat.grad),
+                                                   ("d_data", tr.optimizer_D.flat.data),
+                                                   ("d_grad", tr.optimizer_D.flat.grad))}
+    tr2, _, _ = shard_mean(True)
+    spread = _dp_errors(mid, tr2, g0, d0)
+    print(f"progan {W}-rank: shard mean vs the same with the shards summed in reverse:", spread)
+    for k in ("g_grad", "d_grad", "g_data", "d_data", "g_move", "d_move"):
+        assert errs[k] <= max(3 * spread[k], 1e-5), (k, errs, spread)
 
 
 @pytest.mark.parametrize("mode", ["eager", "graph"])
