@@ -2481,7 +2481,11 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
         dgrad_phase(d, q, &Tq, &kw, &hq, &wq);
         slabs = std::max(slabs, slab_bytes(M, d->B * hq * wq, Ck, Tq, kPhase, d->math == GANAMD_MATH_BF16));
       }
-    *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T, pack_x3(d, op)))) + align256(dgrad_pad_bytes(d)) +
+    // the packed copy as ganamd_conv_dgrad lays it out: a_operand's shape (the phased form packs
+    // all s*s phases, KH*KW taps in all -- not phase 0's, which sized the GEMM above)
+    int Ma, Cka, Ta, sma, sca;
+    a_operand(d, GANAMD_CONV_DGRAD, &Ma, &Cka, &Ta, &sma, &sca);
+    *bytes = (d->packed_w ? 0 : align256(pack_bytes(Ma, Cka, Ta, pack_x3(d, op)))) + align256(dgrad_pad_bytes(d)) +
              align256(dgrad_scatter_bytes(d)) + slabs;
   } else if (op == GANAMD_CONV_WGRAD) {
     const int Kpix = d->transposed ? d->B * d->H * d->W : d->B * d->OH * d->OW;

@@ -102,6 +102,14 @@ def test_conv_block_schedule(shape, op):
         assert (pl["S"] - 1) * pl["kt_per_split"] < kt_total <= pl["S"] * pl["kt_per_split"]
         n = _lib.c_size_t(0)
         assert _lib.LIB.ganamd_conv_workspace(geo.desc(), op, n) == 0
+        # the unpacked call packs the weights into the workspace first: the whole packed copy must
+        # fit (the phased dgrad packs all s*s phases -- a round-4 bug sized it for phase 0 alone)
+        pb, nraw, npre = _lib.c_size_t(0), _lib.c_size_t(0), _lib.c_size_t(0)
+        raw, pre = geo.desc(packed=False), geo.desc(packed=True)
+        assert _lib.LIB.ganamd_conv_pack_bytes(raw, op, pb) == 0
+        assert _lib.LIB.ganamd_conv_workspace(raw, op, nraw) == 0
+        assert _lib.LIB.ganamd_conv_workspace(pre, op, npre) == 0
+        assert nraw.value - npre.value >= pb.value, (nraw.value, npre.value, pb.value)
         if pl["S"] > 1:
             tail_cols = (geo.B * (geo.OH * geo.OW if op == 0 else 1)) - pl["nfull_t"] * pl["bn"]
             if op == 0:
