@@ -26,12 +26,13 @@ EPI_STORE, EPI_BIAS, EPI_DEMOD, EPI_ACCUM, EPI_SCALE = 0, 1, 2, 3, 4
 CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
 ACT_SIGMOID, ACT_TANH, ACT_LEAKY = 0, 1, 2
 MATH_F32, MATH_BF16 = 0, 1
+KERNEL_PATCH_FWD, KERNEL_PATCH_DGRAD, KERNEL_WGRAD_ROW = 1, 2, 4     # ganamd_conv_desc.kernel_off bits
 
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("B", "Cin", "H", "W", "Cout", "OH", "OW", "KH", "KW", "stride", "pad", "pad_mode", "transposed",
-                 "packed_w", "math")]
+                 "packed_w", "math", "kernel_off")]
 
 
 class GTile(ctypes.Structure):
@@ -70,34 +71,34 @@ _SIGS = {
     "ganamd_stream_capture_id": (c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong)]),
     "ganamd_conv_workspace": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_plan_info": (c_int, [ctypes.POINTER(ConvDesc), c_int, c_int, ctypes.POINTER(ctypes.c_int)]),
-    "ganamd_conv_set_patch": (c_int, [c_int]),
     "ganamd_conv_pack_bytes": (c_int, [ctypes.POINTER(ConvDesc), c_int, ctypes.POINTER(c_size_t)]),
     "ganamd_conv_pack_job": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, ctypes.POINTER(PackJob)]),
     "ganamd_pack_job_chunks": (ctypes.c_int64, [ctypes.POINTER(PackJob)]),
     "ganamd_conv_pack_batch": (c_int, [vp, c_int, ctypes.c_int64, vp]),
     "ganamd_conv_pack": (c_int, [ctypes.POINTER(ConvDesc), c_int, vp, vp, vp]),
-    "ganamd_conv_fwd_ex": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp, vp, vp, vp]),
+    "ganamd_conv_fwd_ex": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp, vp, vp, c_size_t,
+                                   vp]),
     "ganamd_mix_fwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp]),
     "ganamd_mix_bwd": (c_int, [c_int, vp, vp, vp, vp, vp, c_long, c_long, vp, vp, vp, vp, vp, vp, vp]),
     "ganamd_gp_workspace": (c_size_t, [c_int, c_long]),
-    "ganamd_gp_fwd": (c_int, [vp, c_int, c_long, c_float, c_float, c_int, vp, vp, vp, vp]),
+    "ganamd_gp_fwd": (c_int, [vp, c_int, c_long, c_float, c_float, c_int, vp, vp, vp, c_size_t, vp]),
     "ganamd_gp_bwd": (c_int, [vp, vp, vp, c_int, c_long, c_float, c_float, c_int, vp, vp]),
     "ganamd_add_prelu": (c_int, [vp, vp, vp, c_int, c_long, vp, vp]),
     "ganamd_modconv_sd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_long, vp, vp, vp, vp]),
     "ganamd_route_bwd": (c_int, [c_int, vp, vp, vp, c_int, c_long, vp, vp]),
     "ganamd_scale_add": (c_int, [vp, vp, vp, c_long, c_long, vp, vp]),
-    "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, vp]),
-    "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp]),
-    "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
-    "ganamd_conv_wgrad2": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, vp]),
+    "ganamd_conv_fwd": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, vp, c_float, vp, vp, c_size_t, vp]),
+    "ganamd_conv_dgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, c_size_t, vp]),
+    "ganamd_conv_wgrad": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, c_size_t, vp]),
+    "ganamd_conv_wgrad2": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, vp, c_float, vp, c_int, vp, c_size_t, vp]),
     "ganamd_rowreduce_workspace": (c_size_t, [c_int, c_long]),
-    "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, vp]),
+    "ganamd_bn_act_fwd": (c_int, [vp, c_int, c_long, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp, c_size_t, vp]),
     "ganamd_bn_act_fwd_seg": (c_int, [vp, c_int, c_long, c_int, vp, vp, vp, vp, vp, c_float, c_float, vp, vp, vp, vp,
-                                      vp, vp]),
-    "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp]),
+                                      vp, c_size_t, vp]),
+    "ganamd_bn_act_bwd": (c_int, [vp, vp, c_int, c_long, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_size_t, vp]),
     "ganamd_prelu_fwd": (c_int, [vp, vp, c_int, c_long, vp, vp]),
-    "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),
-    "ganamd_prelu_bwd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_long, vp, vp, vp, vp, vp]),
+    "ganamd_prelu_bwd": (c_int, [vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, c_size_t, vp]),
+    "ganamd_prelu_bwd_bwd": (c_int, [vp, vp, vp, vp, vp, c_int, c_long, vp, vp, vp, vp, c_size_t, vp]),
     "ganamd_resample2d": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int, vp]),
     "ganamd_resample2d_add": (c_int, [vp, c_long, c_int, c_int, vp, c_int, c_int, vp, vp, c_int, vp, vp, c_int,
                                       vp, vp, vp, vp]),
@@ -105,11 +106,11 @@ _SIGS = {
                                       vp]),
     "ganamd_plane_dot_pair": (c_int, [vp, vp, vp, c_long, c_long, vp, vp, vp]),
     "ganamd_plane_dot": (c_int, [vp, vp, c_long, c_long, c_float, vp, vp]),
-    "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, c_int, vp, vp]),
+    "ganamd_row_dot": (c_int, [vp, vp, c_int, c_long, vp, c_int, vp, c_size_t, vp]),
     "ganamd_segment_sumsq": (c_int, [vp, c_long, c_int, vp, vp]),
     "ganamd_adamw": (c_int, [vp, vp, vp, vp, c_long, vp, c_float, c_float, c_float, c_float, c_float, vp]),
     "ganamd_grouped_gemm": (c_int, [vp, vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp]),
-    "ganamd_prelu_tangent": (c_int, [vp, vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, vp]),
+    "ganamd_prelu_tangent": (c_int, [vp, vp, vp, vp, c_int, c_long, vp, vp, c_int, vp, c_size_t, vp]),
     "ganamd_act_fwd": (c_int, [c_int, vp, c_long, c_float, vp, vp]),
     "ganamd_act_bwd": (c_int, [c_int, vp, vp, c_long, c_float, vp, vp]),
     "ganamd_act_adjoint": (c_int, [c_int, vp, vp, vp, vp, c_long, c_float, vp, vp]),
@@ -121,30 +122,31 @@ _SIGS = {
     "ganamd_softmax_m": (c_int, [c_int, vp, c_long, vp, vp]),
     "ganamd_softmax_m_bwd": (c_int, [c_int, vp, vp, c_long, vp, vp]),
     "ganamd_mbstd_workspace": (c_size_t, [c_int]),
-    "ganamd_mbstd_fwd": (c_int, [vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, vp, vp]),
-    "ganamd_mbstd_bwd": (c_int, [vp, c_long, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, vp]),
-    "ganamd_mbstd_tangent": (c_int, [vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, vp]),
-    "ganamd_mbstd_adjoint": (c_int, [vp, vp, c_long, vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, vp]),
+    "ganamd_mbstd_fwd": (c_int, [vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, vp, c_size_t, vp]),
+    "ganamd_mbstd_bwd": (c_int, [vp, c_long, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, c_size_t, vp]),
+    "ganamd_mbstd_tangent": (c_int, [vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, c_long, vp, c_size_t, vp]),
+    "ganamd_mbstd_adjoint": (c_int, [vp, vp, c_long, vp, vp, c_long, c_int, c_int, c_int, c_int, c_int, vp, vp, c_size_t,
+                                     vp]),
     "ganamd_linear_bn_act": (c_int, [ctypes.POINTER(ConvDesc), vp, vp, vp, c_float, vp, vp, vp, vp, vp, c_float, c_float,
-                                     vp, vp, vp]),
+                                     vp, vp, c_size_t, vp]),
     "ganamd_philox_uniform": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_normal": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_draw": (c_int, [vp, c_long, ctypes.c_uint64, vp, ctypes.c_uint32, c_int, c_int, vp]),
     "ganamd_philox_advance": (c_int, [vp, vp]),
-    "ganamd_critic_create": (vp, [ctypes.POINTER(CriticOp), c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "ganamd_critic_create": (vp, [ctypes.POINTER(CriticOp), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "ganamd_critic_destroy": (None, [vp]),
     "ganamd_critic_workspace": (c_int, [vp, ctypes.POINTER(c_size_t)]),
     "ganamd_critic_value": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ganamd_critic_region_bytes": (c_int, [vp, c_int, ctypes.POINTER(c_size_t)]),
-    "ganamd_critic_bind": (c_int, [vp, c_int, vp]),
-    "ganamd_critic_forward": (c_int, [vp, vp, vp, vp, vp]),
-    "ganamd_critic_backward": (c_int, [vp, vp, vp, vp, vp, vp]),
-    "ganamd_critic_tangent": (c_int, [vp, vp, vp, vp, vp]),
-    "ganamd_critic_adjoint": (c_int, [vp, vp, vp, vp, vp, vp]),
-    "ganamd_critic_gp_step": (c_int, [vp, vp, c_float, c_float, c_int, vp, vp, vp, vp, vp, vp, vp]),
+    "ganamd_critic_bind": (c_int, [vp, c_int, vp, c_size_t]),
+    "ganamd_critic_forward": (c_int, [vp, vp, vp, vp, c_size_t, vp]),
+    "ganamd_critic_backward": (c_int, [vp, vp, vp, vp, vp, c_size_t, vp]),
+    "ganamd_critic_tangent": (c_int, [vp, vp, vp, vp, c_size_t, vp]),
+    "ganamd_critic_adjoint": (c_int, [vp, vp, vp, vp, vp, c_size_t, vp]),
+    "ganamd_critic_gp_step": (c_int, [vp, vp, c_float, c_float, c_int, vp, vp, vp, vp, vp, vp, c_size_t, vp]),
     "ganamd_image_batch_workspace": (c_size_t, [c_int, c_int, c_int]),
     "ganamd_image_batch": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, c_int, c_int, vp, vp, c_int, c_int, vp, vp,
-                                   vp, vp, vp]),
+                                   vp, vp, c_size_t, vp]),
 }
 
 EXPORTS = tuple(_SIGS)
@@ -198,6 +200,13 @@ def iptr(t):
 def workspace(nbytes: int, device) -> torch.Tensor:
     """Caller-provided scratch from torch's caching allocator (graph-capture safe)."""
     return torch.empty(max(int(nbytes), 4) // 4 + 1, dtype=torch.float32, device=device)
+
+
+def ws(t):
+    """(pointer, bytes) of a workspace tensor (None -> NULL, 0): the two workspace arguments of the ABI."""
+    if t is None:
+        return None, 0
+    return ptr(t), t.numel() * t.element_size()
 
 
 def capture_id() -> int:

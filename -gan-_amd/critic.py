@@ -49,6 +49,7 @@ from torch.autograd import Function
 
 from . import _lib, ops, tables
 from ._lib import LIB, check, ptr, stream, workspace
+from ._lib import ws as wsarg
 
 # ------------------------------------------------------------------------------------------
 # program
@@ -308,7 +309,8 @@ class Run:
             self.vec[op.out] = op.kind in ("linear", "pmean", "flatten") or (
                 op.kind in ("prelu", "sigmoid") and self.vec[op.ins[0]])
         self.table = _op_table(self.prog, B, self.sh, x.device, self.keep)
-        self.plan = LIB.ganamd_critic_create(self.table, len(self.prog.ops), B, C, H, W, self.segments, ops._MATH[0])
+        self.plan = LIB.ganamd_critic_create(self.table, len(self.prog.ops), B, C, H, W, self.segments, ops._MATH[0],
+                                             ops._KOFF[0])
         if not self.plan:
             raise _lib.GanAmdError(f"critic program rejected by ganamd_critic_create (B={B}, segments={self.segments})")
         self._region(0, x.device)
@@ -319,7 +321,7 @@ class Run:
             n = _lib.c_size_t(0)
             check(LIB.ganamd_critic_region_bytes(self.plan, which, _lib.ctypes.byref(n)), "critic_region_bytes")
             self.regions[which] = workspace(n.value, device)
-            check(LIB.ganamd_critic_bind(self.plan, which, ptr(self.regions[which])), "critic_bind")
+            check(LIB.ganamd_critic_bind(self.plan, which, *wsarg(self.regions[which])), "critic_bind")
 
     def _grads(self):
         """ganamd_critic_grads[] of the parameters that want a gradient (created as zeros)."""
@@ -367,7 +369,7 @@ class Run:
         self.x = x_nchw
         self._setup(x_nchw)
         self._count("forward")
-        check(LIB.ganamd_critic_forward(self.plan, ptr(x_nchw), None, None, stream()), "critic_forward")
+        check(LIB.ganamd_critic_forward(self.plan, ptr(x_nchw), None, None, 0, stream()), "critic_forward")
         return self.X[self.prog.out].clone()               # [1, B], not a view of the workspace
 
     def backward(self, seed, params: bool, need_input: bool):
@@ -378,7 +380,7 @@ class Run:
         gx = torch.empty_like(self.x) if need_input else None
         self._region(1, self.x.device)
         check(LIB.ganamd_critic_backward(self.plan, ptr(self.seed), self._grads() if params else None, ptr(gx),
-                                         None, stream()), "critic_backward")
+                                         None, 0, stream()), "critic_backward")
         return gx
 
     def tangent(self, v_nchw, params: bool):
@@ -387,7 +389,7 @@ class Run:
         self._count("tangent")
         self.v = v_nchw.contiguous()
         self._region(2, self.x.device)
-        check(LIB.ganamd_critic_tangent(self.plan, ptr(self.v), self._grads() if params else None, None,
+        check(LIB.ganamd_critic_tangent(self.plan, ptr(self.v), self._grads() if params else None, None, 0,
                                         stream()), "critic_tangent")
         return self.XD[self.prog.out]
 
@@ -399,7 +401,7 @@ class Run:
         ax = torch.empty_like(self.x) if need_input else None
         self._region(3, self.x.device)
         check(LIB.ganamd_critic_adjoint(self.plan, ptr(self.a_seed), self._grads() if params else None, ptr(ax),
-                                        None, stream()), "critic_adjoint")
+                                        None, 0, stream()), "critic_adjoint")
         return ax
 
 # ------------------------------------------------------------------------------------------
@@ -414,7 +416,7 @@ def _penalty(g, center, lam, mode):
     norms = torch.empty(B, device=g.device, dtype=torch.float32)
     out = torch.empty((), device=g.device, dtype=torch.float32)
     ws = workspace(LIB.ganamd_gp_workspace(B, n), g.device)
-    check(LIB.ganamd_gp_fwd(ptr(g), B, n, float(center), float(lam), int(mode), ptr(norms), ptr(out), ptr(ws),
+    check(LIB.ganamd_gp_fwd(ptr(g), B, n, float(center), float(lam), int(mode), ptr(norms), ptr(out), *wsarg(ws),
                             stream()), "gp_fwd")
     return out, norms
 

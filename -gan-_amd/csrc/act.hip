@@ -446,9 +446,9 @@ int ganamd_softmax_m_bwd(int M, const float* y, const float* gy, long P, float* 
 size_t ganamd_mbstd_workspace(int S) { return sizeof(double) * (size_t)std::max(1, S) * (kMbBlocks + 2); }
 
 int ganamd_mbstd_fwd(const float* x, long ldx, int C, int B, int HW, int S, int G, float* y, long ldy, float* std_out,
-                     void* ws, hipStream_t st) {
+                     void* ws, size_t ws_bytes, hipStream_t st) {
   const MbGeo g{C, B, HW, S, G, ldx, ldy};
-  if (!x || !y || !ws || !mb_ok(g)) return GANAMD_EINVAL;
+  if (!x || !y || !ws || !mb_ok(g) || ws_bytes < ganamd_mbstd_workspace(S)) return GANAMD_EINVAL;
   const int nb = mb_chunks(g);
   const long n = (long)(B / S / G) * C * HW;
   double* part = static_cast<double*>(ws);
@@ -458,9 +458,9 @@ int ganamd_mbstd_fwd(const float* x, long ldx, int C, int B, int HW, int S, int 
 }
 
 int ganamd_mbstd_bwd(const float* x, long ldx, const float* gy, long ldy, int C, int B, int HW, int S, int G,
-                     float* gx, void* ws, hipStream_t st) {
+                     float* gx, void* ws, size_t ws_bytes, hipStream_t st) {
   const MbGeo g{C, B, HW, S, G, ldx, ldy};
-  if (!x || !gy || !gx || !ws || !mb_ok(g)) return GANAMD_EINVAL;
+  if (!x || !gy || !gx || !ws || !mb_ok(g) || ws_bytes < ganamd_mbstd_workspace(S)) return GANAMD_EINVAL;
   double* sums = static_cast<double*>(ws);
   hipLaunchKernelGGL(mbstd_rowsum_kernel, dim3(S), dim3(kNT), 0, st, g, gy, nullptr, sums);
   hipLaunchKernelGGL(mbstd_back_kernel<4>, dim3(mb_chunks(g), S), dim3(kNT), 0, st, g, x, nullptr, gy, sums, gx);
@@ -468,9 +468,9 @@ int ganamd_mbstd_bwd(const float* x, long ldx, const float* gy, long ldy, int C,
 }
 
 int ganamd_mbstd_tangent(const float* x, const float* xd, long ldx, int C, int B, int HW, int S, int G, float* yd,
-                         long ldy, void* ws, hipStream_t st) {
+                         long ldy, void* ws, size_t ws_bytes, hipStream_t st) {
   const MbGeo g{C, B, HW, S, G, ldx, ldy};
-  if (!x || !xd || !yd || !ws || !mb_ok(g)) return GANAMD_EINVAL;
+  if (!x || !xd || !yd || !ws || !mb_ok(g) || ws_bytes < ganamd_mbstd_workspace(S)) return GANAMD_EINVAL;
   const int nb = mb_chunks(g);
   const long n = (long)(B / S / G) * C * HW;
   double* part = static_cast<double*>(ws);
@@ -481,9 +481,10 @@ int ganamd_mbstd_tangent(const float* x, const float* xd, long ldx, int C, int B
 }
 
 int ganamd_mbstd_adjoint(const float* x, const float* xd, long ldx, const float* gy, const float* ay, long ldy, int C,
-                         int B, int HW, int S, int G, float* ax, void* ws, hipStream_t st) {
+                         int B, int HW, int S, int G, float* ax, void* ws, size_t ws_bytes, hipStream_t st) {
   const MbGeo g{C, B, HW, S, G, ldx, ldy};
-  if (!x || !xd || !gy || !ay || !ax || !ws || !mb_ok(g)) return GANAMD_EINVAL;
+  if (!x || !xd || !gy || !ay || !ax || !ws || !mb_ok(g) || ws_bytes < ganamd_mbstd_workspace(S))
+    return GANAMD_EINVAL;
   double* sums = static_cast<double*>(ws);
   hipLaunchKernelGGL(mbstd_rowsum_kernel, dim3(S), dim3(kNT), 0, st, g, gy, ay, sums);
   hipLaunchKernelGGL(mbstd_back_kernel<4>, dim3(mb_chunks(g), S), dim3(kNT), 0, st, g, x, xd, ay, sums, ax);

@@ -2053,10 +2053,9 @@ hipError_t launch_linear(const ConvArgs& p, hipStream_t st) {
 }
 
 // ---- the split6 LDS-patch conv (conv_patch.hip) and row-blocked wgrad (conv_wgrad_row.hip) ------
-// bit 0: forward, bit 1: dgrad interior through the patch conv where its domain and grid fit, bit 2:
-// weight gradients through the row-blocked kernel (ganamd_conv_set_patch: A/B; default all)
-std::atomic<int> g_patch{7};
-int patch_enabled() { return g_patch.load(std::memory_order_relaxed); }
+// Which of them a call may use is the descriptor's kernel_off (GANAMD_KERNEL_*: per call, no library
+// state; 0 = all allowed where their domains and grids fit).
+constexpr int kMaxPatchScaleChannels = 1024;   // conv_patch.hip kMaxScale: scales staged in LDS
 
 // The packed operand carries the three bf16 planes the patch conv reads (after the fp32 copy the
 // gather GEMM reads) whenever the GEMM's geometry is in the patch kernel's domain -- a function of
@@ -2072,10 +2071,14 @@ long patch_blocks(int M, int B, int H, int W) {
   a.W = W;
   return ganamd_patch::blocks(a);
 }
-// ... and where it runs: fp32 math, enabled, and a grid of at least one block per CU whose last
-// round is full or follows another (these long one-per-CU blocks leave a half-empty last round idle)
-bool patch_geometry(int M, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math, bool dgrad) {
-  if (!(patch_enabled() & (dgrad ? 2 : 1)) || math != GANAMD_MATH_F32 || !patch_packed(M, H, W, K, stride, pad, OH, OW))
+// ... and where it runs: fp32 math, allowed by the descriptor, at most kMaxPatchScaleChannels input
+// channels (the modulation scales the block stages in LDS: past that the gather GEMM takes the conv
+// instead of the launch failing), and a grid of at least one block per CU whose last round is full or
+// follows another (these long one-per-CU blocks leave a half-empty last round idle)
+bool patch_geometry(int M, int Ck, int B, int H, int W, int K, int stride, int pad, int OH, int OW, int math,
+                    int kernel_off, bool dgrad) {
+  if ((kernel_off & (dgrad ? GANAMD_KERNEL_PATCH_DGRAD : GANAMD_KERNEL_PATCH_FWD)) || math != GANAMD_MATH_F32 ||
+      Ck > kMaxPatchScaleChannels || !patch_packed(M, H, W, K, stride, pad, OH, OW))
     return false;
   const long blocks = patch_blocks(M, B, H, W), cus = num_cus();
   return blocks >= cus && (blocks % cus == 0 || blocks >= 2 * cus);
@@ -2184,7 +2187,16 @@ bool extents_ok(const ganamd_conv_desc* d) {
 bool desc_ok(const ganamd_conv_desc* d) {
   return d && d->B > 0 && d->Cin > 0 && d->Cout > 0 && d->H > 0 && d->W > 0 && d->OH > 0 && d->OW > 0 &&
          d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0 &&
-         (d->math == GANAMD_MATH_F32 || d->math == GANAMD_MATH_BF16) && extents_ok(d);
+         (d->math == GANAMD_MATH_F32 || d->math == GANAMD_MATH_BF16) &&
+         (d->kernel_off & ~(GANAMD_KERNEL_PATCH_FWD | GANAMD_KERNEL_PATCH_DGRAD | GANAMD_KERNEL_WGRAD_ROW)) == 0 &&
+         extents_ok(d);
+}
+
+// the call's workspace against the query for its descriptor (GANAMD_EINVAL when short or missing)
+int ws_check(const ganamd_conv_desc* d, int op, const void* workspace, size_t workspace_bytes) {
+  size_t need = 0;
+  if (ganamd_conv_workspace(d, op, &need) != GANAMD_OK) return GANAMD_EINVAL;
+  return need && (!workspace || workspace_bytes < need) ? GANAMD_EINVAL : GANAMD_OK;
 }
 
 }  // namespace
@@ -2324,7 +2336,7 @@ static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* 
 // The row-blocked split6 weight gradient (conv_wgrad_row.hip) where its domain fits: fp32 math,
 // stride-1 same convs on 32 / 64-wide maps; the split-K partial sums reduced here.
 static bool wrow_ok(const ganamd_conv_desc* d) {
-  return (patch_enabled() & 4) && d->math == GANAMD_MATH_F32 && d->KH == d->KW &&
+  return !(d->kernel_off & GANAMD_KERNEL_WGRAD_ROW) && d->math == GANAMD_MATH_F32 && d->KH == d->KW &&
          ganamd_wrow::domain(d->Cout, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->transposed);
 }
 static int wrow_splits(const ganamd_conv_desc* d, int segs) {
@@ -2393,12 +2405,6 @@ int ganamd_conv_pack_bytes(const ganamd_conv_desc* d, int op, size_t* bytes) {
   return GANAMD_OK;
 }
 
-int ganamd_conv_set_patch(int mask) {
-  const int prev = patch_enabled();
-  if (mask >= 0) g_patch.store(mask & 7, std::memory_order_relaxed);
-  return prev;
-}
-
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info) {
   if (!desc_ok(d) || !info || (op != GANAMD_CONV_FWD && op != GANAMD_CONV_DGRAD)) return GANAMD_EINVAL;
   int M, N, Ck, T;
@@ -2408,8 +2414,8 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
     dgrad_gemm(d, &M, &N, &Ck, &T);
   const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
   const int Mp = op == GANAMD_CONV_FWD ? d->Cout : d->Cin;
-  if (pack_x3(d, op) && patch_geometry(Mp, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math,
-                                       op == GANAMD_CONV_DGRAD)) {
+  if (pack_x3(d, op) && patch_geometry(Mp, Ck, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math,
+                                       d->kernel_off, op == GANAMD_CONV_DGRAD)) {
     ganamd_patch::Args a{};
     a.M = Mp;
     a.B = d->B;
@@ -2510,21 +2516,20 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
 
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
-                    hipStream_t stream) {
-  return ganamd_conv_fwd_ex(d, x, w, bias, x_scale, y_scale, alpha, nullptr, nullptr, nullptr, y, workspace, stream);
+                    size_t workspace_bytes, hipStream_t stream) {
+  return ganamd_conv_fwd_ex(d, x, w, bias, x_scale, y_scale, alpha, nullptr, nullptr, nullptr, y, workspace,
+                            workspace_bytes, stream);
 }
 
 int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias, float alpha,
                          const float* gamma, const float* beta, const float* act_alpha, float* running_mean,
                          float* running_var, float momentum, float eps, float* y, void* workspace,
-                         hipStream_t stream) {
+                         size_t workspace_bytes, hipStream_t stream) {
   if (!desc_ok(d) || !x || !w || !y || !gamma || !beta || !running_mean || !running_var) return GANAMD_EINVAL;
   if (d->H != 1 || d->W != 1 || d->KH != 1 || d->KW != 1 || d->transposed || d->stride != 1 || d->pad != 0 ||
       d->math != GANAMD_MATH_F32 || d->B < 2 || d->B > 64)
     return GANAMD_EINVAL;
-  size_t need = 0;
-  ganamd_conv_workspace(d, GANAMD_CONV_FWD, &need);
-  if (need && !d->packed_w && !workspace) return GANAMD_EINVAL;
+  if (!d->packed_w && ws_check(d, GANAMD_CONV_FWD, workspace, workspace_bytes) != GANAMD_OK) return GANAMD_EINVAL;
   ConvArgs p{};
   p.M = d->Cout;
   p.Ck = d->Cin;
@@ -2559,11 +2564,9 @@ int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float*
 int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                        const float* x_scale, const float* y_scale, float alpha, const float* noise,
                        const float* noise_scale, const float* act_alpha, float* y, void* workspace,
-                       hipStream_t stream) {
+                       size_t workspace_bytes, hipStream_t stream) {
   if (!desc_ok(d) || !x || !w || !y || (noise && !noise_scale)) return GANAMD_EINVAL;
-  size_t need = 0;
-  ganamd_conv_workspace(d, GANAMD_CONV_FWD, &need);
-  if (need && !workspace) return GANAMD_EINVAL;
+  if (ws_check(d, GANAMD_CONV_FWD, workspace, workspace_bytes) != GANAMD_OK) return GANAMD_EINVAL;
   ConvArgs p{};
   int M, N, Ck, T, sm, sc;
   fwd_gemm(d, &M, &N, &Ck, &T);
@@ -2593,7 +2596,7 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
   float* packed = d->packed_w ? nullptr : reinterpret_cast<float*>(ws);
   float* slab = reinterpret_cast<float*>(ws + (d->packed_w ? 0 : align256(pack_bytes(M, Ck, T, pack_x3(d, GANAMD_CONV_FWD)))));
   if (pack_x3(d, GANAMD_CONV_FWD) &&
-      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, false)) {
+      patch_geometry(M, Ck, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, d->kernel_off, false)) {
     // the split6 LDS-patch conv (conv_patch.hip) on the planes of the packed operand
     const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
     p.Ckp = (Ck + BK - 1) / BK * BK;
@@ -2635,11 +2638,9 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
 }
 
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale, float alpha,
-                      float* gx, void* workspace, hipStream_t stream) {
+                      float* gx, void* workspace, size_t workspace_bytes, hipStream_t stream) {
   if (!desc_ok(d) || !gy || !w || !gx) return GANAMD_EINVAL;
-  size_t need = 0;
-  ganamd_conv_workspace(d, GANAMD_CONV_DGRAD, &need);
-  if (need && !workspace) return GANAMD_EINVAL;
+  if (ws_check(d, GANAMD_CONV_DGRAD, workspace, workspace_bytes) != GANAMD_OK) return GANAMD_EINVAL;
   int M, N, Ck, T, sm, sc;
   dgrad_gemm(d, &M, &N, &Ck, &T);
   a_operand(d, GANAMD_CONV_DGRAD, &M, &Ck, &T, &sm, &sc);
@@ -2729,7 +2730,7 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
   // dropped (zero padding); ring_fold_kernel then adds the ring onto the edge pixels.
   const int Hp = d->H + 2 * d->pad, Wp = d->W + 2 * d->pad;
   if (pack_x3(d, GANAMD_CONV_DGRAD) &&
-      patch_geometry(M, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, true)) {
+      patch_geometry(M, Ck, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math, d->kernel_off, true)) {
     // the frame's interior with the split6 patch conv (zero-padded, taps reversed), then -- for
     // replication padding -- the ring alone through the gather GEMM (OutMap s = -2) and its fold
     const int bmp = conv_bm(M), mpad = (M + bmp - 1) / bmp * bmp;
@@ -2861,9 +2862,10 @@ static int wgrad_row(const ganamd_conv_desc* d, const float* x, const float* gy,
 
 int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
                       const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
-                      hipStream_t stream) {
+                      size_t workspace_bytes, hipStream_t stream) {
   if (!desc_ok(d) || !x || !gy || !gw) return GANAMD_EINVAL;
   if ((x_scale == nullptr) != (gy_scale == nullptr)) return GANAMD_EINVAL;
+  if (ws_check(d, GANAMD_CONV_WGRAD, workspace, workspace_bytes) != GANAMD_OK) return GANAMD_EINVAL;
   if (wrow_ok(d))
     return wgrad_row(d, x, gy, x_scale, gy_scale, nullptr, nullptr, alpha, gw, accumulate, workspace, stream);
   const WgradArgs p = wgrad_args(d, x, gy, x_scale, gy_scale, alpha, gw, accumulate);
@@ -2872,13 +2874,17 @@ int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy
 }
 
 int ganamd_conv_wgrad2(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x2, const float* gy2,
-                       float alpha, float* gw, int accumulate, void* workspace, hipStream_t stream) {
+                       float alpha, float* gw, int accumulate, void* workspace, size_t workspace_bytes,
+                       hipStream_t stream) {
   if (!desc_ok(d) || !x || !gy || !x2 || !gy2 || !gw) return GANAMD_EINVAL;
+  if (ws_check(d, GANAMD_CONV_WGRAD, workspace, workspace_bytes) != GANAMD_OK) return GANAMD_EINVAL;
   if (wrow_ok(d)) return wgrad_row(d, x, gy, nullptr, nullptr, x2, gy2, alpha, gw, accumulate, workspace, stream);
   WgradArgs p = wgrad_args(d, x, gy, nullptr, nullptr, alpha, gw, accumulate);
   if (d->transposed || p.K % BKW != 0 || (long)2 * p.K >= (1L << 31) / 4) {   // two launches instead
-    int rc = ganamd_conv_wgrad(d, x, gy, nullptr, nullptr, alpha, gw, accumulate, workspace, stream);
-    return rc != GANAMD_OK ? rc : ganamd_conv_wgrad(d, x2, gy2, nullptr, nullptr, alpha, gw, 1, workspace, stream);
+    int rc = ganamd_conv_wgrad(d, x, gy, nullptr, nullptr, alpha, gw, accumulate, workspace, workspace_bytes, stream);
+    return rc != GANAMD_OK ? rc
+                           : ganamd_conv_wgrad(d, x2, gy2, nullptr, nullptr, alpha, gw, 1, workspace, workspace_bytes,
+                                               stream);
   }
   p.segK = p.K;
   p.K *= 2;

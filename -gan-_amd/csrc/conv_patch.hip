@@ -48,6 +48,20 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kOOB = (int)0x80000000;
 constexpr int kMaxScale = 1024;   // input channels whose scales the block stages in LDS
 
+// instance shapes (compile-time; tools/build_variant.sh A/B builds override them)
+#ifndef GANAMD_P96_NW
+#define GANAMD_P96_NW 12          // waves of a 96-row block at W = 64
+#endif
+#ifndef GANAMD_P96_MB
+#define GANAMD_P96_MB 32          // MFMA block edge of the 96-row blocks (16: paired 16x16x32)
+#endif
+#ifndef GANAMD_P48_NW
+#define GANAMD_P48_NW 8           // waves of a 48-row block at W = 64
+#endif
+#ifndef GANAMD_P_UNROLL4
+#define GANAMD_P_UNROLL4 1        // fully unroll the tap loop of 4-wave blocks
+#endif
+
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
 }
@@ -101,7 +115,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   // third of the weight fragments per wave, 3 waves per SIMD); otherwise every wave owns all rows
   constexpr int WM = (BM == 96 && NW == 12) ? 3 : 1, WN = NW / WM;
   constexpr int PW = NPIX / WN;                             // pixels per wave
-  constexpr int MB = (BM % 32 == 0) ? 32 : 16;              // MFMA block edge (48 rows: 16)
+  constexpr int MB = (BM % 32 == 0) ? (BM == 96 ? GANAMD_P96_MB : 32) : 16;   // MFMA block edge (48 rows: 16)
   constexpr int TM = BM / (MB * WM), TN = PW / MB, NR = MB == 32 ? 16 : 4;
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
   constexpr int TH = NPIX / TW, PAD = (KK - 1) / 2, T = KK * KK;
@@ -321,7 +335,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
     // blocks: the taps' index math, weight prefetch and patch stores resolve at compile time and the
     // next tap's fragment reads can be scheduled under the current tap's products); the 12-wave 96-row
     // blocks spill when unrolled (or with the first taps peeled) and keep a loop of two taps
-    if constexpr (BM == 48 || NW == 4) {
+    if constexpr (BM == 48 || (NW == 4 && GANAMD_P_UNROLL4)) {
 #pragma unroll
       for (int t = 0; t < T; t += 2) tap_pair(t);
     } else {
@@ -370,7 +384,7 @@ int occ_of() {
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
   if (a.W == 64) {
-    constexpr int NW = BM == 96 ? 12 : 8;
+    constexpr int NW = BM == 96 ? GANAMD_P96_NW : GANAMD_P48_NW;
     if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
       hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),

@@ -93,6 +93,14 @@ int fill(float* p, long n, float v, hipStream_t s) {
 // its graph -- an eager sweep on another stream never touches a stream being captured.  Each plan
 // has its own fork / join events.  Same kernels, same per-buffer accumulation order (all weight
 // gradients of a sweep run in sweep order on the side stream), so results are unchanged.
+// Why this is capture-safe where round 4's penalty-on-a-second-stream path crashed capture_end: here the
+// fork / join are plain hipEventRecord / hipStreamWaitEvent pairs on a library stream, nothing is
+// allocated on it (all memory is the caller's workspace), and every sweep joins before it returns, so
+// a capture never ends with unjoined side-stream work; the removed path ran a PyTorch autograd node's
+// backward on a torch side stream inside the capture (the engine's cross-stream event syncs and
+// caching-allocator blocks on a non-origin stream), which is what brought capture_end down.
+// A stream that cannot be created is remembered as such (no retry per sweep: that caller's sweeps run
+// serially).  Entries live as long as the process (one per caller stream).
 hipStream_t side_stream(hipStream_t caller) {
   struct Entry {
     int dev;
@@ -106,7 +114,7 @@ hipStream_t side_stream(hipStream_t caller) {
   for (const Entry& e : table)
     if (e.dev == dev && e.caller == caller) return e.side;
   hipStream_t side = nullptr;
-  if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) side = nullptr;
   table.push_back(Entry{dev, caller, side});
   return side;
 }
@@ -134,7 +142,7 @@ struct ganamd_critic_plan {
   std::vector<ganamd_critic_op> ops;
   std::vector<Val> val;            // value v = output of op v-1; value 0 = the NCHW input
   std::vector<char> input_only;    // value is the input or a layout copy of it (no gradient needed)
-  int B = 0, S = 1, math = GANAMD_MATH_F32, out = 0;
+  int B = 0, S = 1, math = GANAMD_MATH_F32, kernel_off = 0, out = 0;
   long maxn = 0;
   // workspace layout (bytes), set by ganamd_critic_workspace
   bool sized = false;
@@ -179,6 +187,7 @@ struct ganamd_critic_plan {
     d.transposed = 0;
     d.packed_w = packed ? 1 : 0;
     d.math = math;
+    d.kernel_off = kernel_off;
     return d;
   }
   float* at(size_t off) const { return reinterpret_cast<float*>(R[0] + off); }   // scratch and X
@@ -260,9 +269,10 @@ const float* wd(const ganamd_critic_op& op) { return op.w_dgrad ? op.w_dgrad : o
 
 // need_stage: 0 forward, 1 backward, 2 tangent, 3 adjoint (the sweep that must have run before,
 // and the regions the sweep touches: 0..need_stage)
-int check_ws(Plan& p, void* ws, int need_stage) {
+int check_ws(Plan& p, void* ws, size_t ws_bytes, int need_stage) {
   if (!p.sized) return GANAMD_EINVAL;
   if (ws) {
+    if (ws_bytes < p.total) return GANAMD_EINVAL;
     if (need_stage == 0) {                 // one contiguous workspace: carve the four regions
       p.ws = static_cast<char*>(ws);
       size_t o = 0;
@@ -312,13 +322,15 @@ int join(Plan& p, hipStream_t s) {
 extern "C" {
 
 ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops, int B, int C0, int H0, int W0,
-                                         int segments, int math) {
+                                         int segments, int math, int kernel_off) {
   if (!ops || n_ops <= 0 || B <= 0 || C0 <= 0 || H0 <= 0 || W0 <= 0 || segments <= 0 || B % segments) return nullptr;
+  if (kernel_off & ~(GANAMD_KERNEL_PATCH_FWD | GANAMD_KERNEL_PATCH_DGRAD | GANAMD_KERNEL_WGRAD_ROW)) return nullptr;
   auto* p = new ganamd_critic_plan();
   p->ops.assign(ops, ops + n_ops);
   p->B = B;
   p->S = segments;
   p->math = math;
+  p->kernel_off = kernel_off;
   p->val.resize(n_ops + 1);
   p->input_only.assign(n_ops + 1, 0);
   p->val[0] = Val{C0, H0, W0, (long)C0 * B * H0 * W0};
@@ -485,8 +497,8 @@ int ganamd_critic_region_bytes(const ganamd_critic_plan* p, int which, size_t* b
   return GANAMD_OK;
 }
 
-int ganamd_critic_bind(ganamd_critic_plan* p, int which, void* region) {
-  if (!p || !region || which < 0 || which > 3 || !p->sized) return GANAMD_EINVAL;
+int ganamd_critic_bind(ganamd_critic_plan* p, int which, void* region, size_t region_bytes) {
+  if (!p || !region || which < 0 || which > 3 || !p->sized || region_bytes < p->rsz[which]) return GANAMD_EINVAL;
   if (which == 0) {                         // a new evaluation in bound mode
     p->ws = nullptr;
     for (char*& r : p->R) r = nullptr;
@@ -505,9 +517,10 @@ int ganamd_critic_value(const ganamd_critic_plan* p, int which, int v, const flo
   return GANAMD_OK;
 }
 
-int ganamd_critic_forward(ganamd_critic_plan* p, const float* x, float* out, void* workspace, hipStream_t s) {
+int ganamd_critic_forward(ganamd_critic_plan* p, const float* x, float* out, void* workspace, size_t workspace_bytes,
+                          hipStream_t s) {
   if (!p || !x) return GANAMD_EINVAL;
-  TRY(check_ws(*p, workspace, 0));
+  TRY(check_ws(*p, workspace, workspace_bytes, 0));
   p->stage = 0;
   p->X[0] = const_cast<float*>(x);
   for (int i = 0; i < (int)p->ops.size(); ++i) {
@@ -521,7 +534,7 @@ int ganamd_critic_forward(ganamd_critic_plan* p, const float* x, float* out, voi
       case GANAMD_COP_SWAP: TRY(swap_in(*p, in, y, s)); break;
       case GANAMD_COP_CONV: {
         ganamd_conv_desc d = p->desc(i, op.w_fwd != nullptr);
-        TRY(ganamd_conv_fwd(&d, in, wf(op), op.bias, nullptr, nullptr, op.alpha, y, p->at(p->off_conv), s));
+        TRY(ganamd_conv_fwd(&d, in, wf(op), op.bias, nullptr, nullptr, op.alpha, y, p->at(p->off_conv), p->conv_ws, s));
         break;
       }
       case GANAMD_COP_PRELU: TRY(ganamd_prelu_fwd(in, op.w, xv.C, L, y, s)); break;
@@ -536,7 +549,7 @@ int ganamd_critic_forward(ganamd_critic_plan* p, const float* x, float* out, voi
                               (long)xv.C * p->B, xv.hw(), y, s));
         break;
       case GANAMD_COP_MBSTD:
-        TRY(ganamd_mbstd_fwd(in, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, y, L, nullptr, p->at(p->off_mb), s));
+        TRY(ganamd_mbstd_fwd(in, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, y, L, nullptr, p->at(p->off_mb), p->mb_ws, s));
         break;
       case GANAMD_COP_FLATTEN: TRY(flatten(*p, xv, in, y, s)); break;
     }
@@ -548,9 +561,9 @@ int ganamd_critic_forward(ganamd_critic_plan* p, const float* x, float* out, voi
 }
 
 int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganamd_critic_grads* gr, float* gx,
-                           void* workspace, hipStream_t s) {
+                           void* workspace, size_t workspace_bytes, hipStream_t s) {
   if (!p) return GANAMD_EINVAL;
-  TRY(check_ws(*p, workspace, 1));
+  TRY(check_ws(*p, workspace, workspace_bytes, 1));
   Sweep& G = p->G;
   G.reset();
   for (int v = 1; v < (int)p->val.size(); ++v) G.own[v] = p->atr(1, p->offG[v]);
@@ -580,7 +593,7 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
         if (!p->input_only[u] || gx) {
           ganamd_conv_desc d = p->desc(i, op.w_dgrad != nullptr);
           TRY(acc(*p, G, u, [&](float* dst) {
-            return ganamd_conv_dgrad(&d, gy, wd(op), nullptr, op.alpha, dst, p->at(p->off_conv), s);
+            return ganamd_conv_dgrad(&d, gy, wd(op), nullptr, op.alpha, dst, p->at(p->off_conv), p->conv_ws, s);
           }, s));
         }
         const Val& yv = p->val[v];
@@ -589,16 +602,16 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
           const bool sd = ws != s;
           if (gw) {
             ganamd_conv_desc d = p->desc(i, false);
-            TRY(ganamd_conv_wgrad(&d, x, gy, nullptr, nullptr, op.alpha, gw, 1, p->at(sd ? p->off_conv2 : p->off_conv),
+            TRY(ganamd_conv_wgrad(&d, x, gy, nullptr, nullptr, op.alpha, gw, 1, p->at(sd ? p->off_conv2 : p->off_conv), p->conv_ws,
                                   ws));
           }
-          if (gb) TRY(ganamd_row_dot(gy, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(sd ? p->off_rr2 : p->off_rr), ws));
+          if (gb) TRY(ganamd_row_dot(gy, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(sd ? p->off_rr2 : p->off_rr), p->rr_ws, ws));
         }
         break;
       }
       case GANAMD_COP_PRELU:
         TRY(acc(*p, G, u, [&](float* dst) {
-          return ganamd_prelu_bwd(gy, x, op.w, xv.C, L, dst, gw, 1, p->at(p->off_rr), s);
+          return ganamd_prelu_bwd(gy, x, op.w, xv.C, L, dst, gw, 1, p->at(p->off_rr), p->rr_ws, s);
         }, s));
         break;
       case GANAMD_COP_RESAMPLE:
@@ -633,7 +646,7 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
       }
       case GANAMD_COP_MBSTD:
         TRY(acc(*p, G, u, [&](float* dst) {
-          return ganamd_mbstd_bwd(x, L, gy, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, dst, p->at(p->off_mb), s);
+          return ganamd_mbstd_bwd(x, L, gy, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, dst, p->at(p->off_mb), p->mb_ws, s);
         }, s));
         break;
       case GANAMD_COP_FLATTEN:
@@ -647,9 +660,9 @@ int ganamd_critic_backward(ganamd_critic_plan* p, const float* seed, const ganam
 }
 
 int ganamd_critic_tangent(ganamd_critic_plan* p, const float* vdir, const ganamd_critic_grads* gr, void* workspace,
-                          hipStream_t s) {
+                          size_t workspace_bytes, hipStream_t s) {
   if (!p || !vdir) return GANAMD_EINVAL;
-  TRY(check_ws(*p, workspace, 2));
+  TRY(check_ws(*p, workspace, workspace_bytes, 2));
   p->XD[0] = const_cast<float*>(vdir);
   for (int i = 0; i < (int)p->ops.size(); ++i) {
     const ganamd_critic_op& op = p->ops[i];
@@ -663,13 +676,13 @@ int ganamd_critic_tangent(ganamd_critic_plan* p, const float* vdir, const ganamd
       case GANAMD_COP_SWAP: TRY(swap_in(*p, xd, y, s)); break;
       case GANAMD_COP_CONV: {
         ganamd_conv_desc d = p->desc(i, op.w_fwd != nullptr);
-        TRY(ganamd_conv_fwd(&d, xd, wf(op), nullptr, nullptr, nullptr, op.alpha, y, p->at(p->off_conv), s));
+        TRY(ganamd_conv_fwd(&d, xd, wf(op), nullptr, nullptr, nullptr, op.alpha, y, p->at(p->off_conv), p->conv_ws, s));
         break;
       }
       case GANAMD_COP_PRELU: {
         float* gy = p->G.cur[v];
         float* gw = (gr && gy) ? gr[i].gw : nullptr;
-        TRY(ganamd_prelu_tangent(xd, gy ? gy : xd, x, op.w, xv.C, L, y, gw, 1, p->at(p->off_rr), s));
+        TRY(ganamd_prelu_tangent(xd, gy ? gy : xd, x, op.w, xv.C, L, y, gw, 1, p->at(p->off_rr), p->rr_ws, s));
         break;
       }
       case GANAMD_COP_RESAMPLE: TRY(resample(*p, op, xv, xd, y, false, s)); break;
@@ -685,7 +698,7 @@ int ganamd_critic_tangent(ganamd_critic_plan* p, const float* vdir, const ganamd
         break;
       }
       case GANAMD_COP_MBSTD:
-        TRY(ganamd_mbstd_tangent(x, xd, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, y, L, p->at(p->off_mb), s));
+        TRY(ganamd_mbstd_tangent(x, xd, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, y, L, p->at(p->off_mb), p->mb_ws, s));
         break;
       case GANAMD_COP_FLATTEN: TRY(flatten(*p, xv, xd, y, s)); break;
     }
@@ -696,9 +709,9 @@ int ganamd_critic_tangent(ganamd_critic_plan* p, const float* vdir, const ganamd
 }
 
 int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const ganamd_critic_grads* gr, float* ax,
-                          void* workspace, hipStream_t s) {
+                          void* workspace, size_t workspace_bytes, hipStream_t s) {
   if (!p) return GANAMD_EINVAL;
-  TRY(check_ws(*p, workspace, 3));
+  TRY(check_ws(*p, workspace, workspace_bytes, 3));
   Sweep& A = p->A;
   A.reset();
   for (int v = 1; v < (int)p->val.size(); ++v) A.own[v] = p->atr(3, p->offA[v]);
@@ -725,7 +738,7 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
         if (ay && (!p->input_only[u] || ax)) {
           ganamd_conv_desc d = p->desc(i, op.w_dgrad != nullptr);
           TRY(acc(*p, A, u, [&](float* dst) {
-            return ganamd_conv_dgrad(&d, ay, wd(op), nullptr, op.alpha, dst, p->at(p->off_conv), s);
+            return ganamd_conv_dgrad(&d, ay, wd(op), nullptr, op.alpha, dst, p->at(p->off_conv), p->conv_ws, s);
           }, s));
         }
         ganamd_conv_desc d = p->desc(i, false);
@@ -735,11 +748,11 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
           const hipStream_t ws = wstream(*p, s);
           float* cw = p->at(ws != s ? p->off_conv2 : p->off_conv);
           if (gw && ay && gy)
-            TRY(ganamd_conv_wgrad2(&d, x, ay, p->XD[u], gy, op.alpha, gw, 1, cw, ws));
+            TRY(ganamd_conv_wgrad2(&d, x, ay, p->XD[u], gy, op.alpha, gw, 1, cw, p->conv_ws, ws));
           else if (gw)
-            TRY(ganamd_conv_wgrad(&d, ay ? x : p->XD[u], ay ? ay : gy, nullptr, nullptr, op.alpha, gw, 1, cw, ws));
+            TRY(ganamd_conv_wgrad(&d, ay ? x : p->XD[u], ay ? ay : gy, nullptr, nullptr, op.alpha, gw, 1, cw, p->conv_ws, ws));
           if (gb && ay)
-            TRY(ganamd_row_dot(ay, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(ws != s ? p->off_rr2 : p->off_rr),
+            TRY(ganamd_row_dot(ay, nullptr, yv.C, (long)p->B * yv.hw(), gb, 1, p->at(ws != s ? p->off_rr2 : p->off_rr), p->rr_ws,
                                ws));
         }
         break;
@@ -747,7 +760,7 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
       case GANAMD_COP_PRELU:
         if (ay)
           TRY(acc(*p, A, u, [&](float* dst) {
-            return ganamd_prelu_bwd(ay, x, op.w, xv.C, L, dst, gw, 1, p->at(p->off_rr), s);
+            return ganamd_prelu_bwd(ay, x, op.w, xv.C, L, dst, gw, 1, p->at(p->off_rr), p->rr_ws, s);
           }, s));
         break;
       case GANAMD_COP_RESAMPLE:
@@ -811,13 +824,13 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
         }
         if (!gy) {
           TRY(acc(*p, A, u, [&](float* dst) {
-            return ganamd_mbstd_bwd(x, L, ay, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, dst, p->at(p->off_mb), s);
+            return ganamd_mbstd_bwd(x, L, ay, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, dst, p->at(p->off_mb), p->mb_ws, s);
           }, s));
           break;
         }
         TRY(acc(*p, A, u, [&](float* dst) {
           return ganamd_mbstd_adjoint(x, p->XD[u], L, gy, ay, L, xv.C, p->B, (int)xv.hw(), p->S, op.group, dst,
-                                      p->at(p->off_mb), s);
+                                      p->at(p->off_mb), p->mb_ws, s);
         }, s));
         break;
       }
@@ -831,20 +844,20 @@ int ganamd_critic_adjoint(ganamd_critic_plan* p, const float* a_seed, const gana
 
 int ganamd_critic_gp_step(ganamd_critic_plan* p, const float* x, float center, float lambda, int mode,
                           const ganamd_critic_grads* gr, float* out, float* gx, float* norms, float* penalty,
-                          void* workspace, hipStream_t s) {
+                          void* workspace, size_t workspace_bytes, hipStream_t s) {
   if (!p || !x || !penalty || (mode != 0 && mode != 1)) return GANAMD_EINVAL;
-  TRY(ganamd_critic_forward(p, x, out, workspace, s));
+  TRY(ganamd_critic_forward(p, x, out, workspace, workspace_bytes, s));
   float* g = gx ? gx : p->at(p->off_g0);
-  TRY(ganamd_critic_backward(p, nullptr, nullptr, g, workspace, s));
+  TRY(ganamd_critic_backward(p, nullptr, nullptr, g, workspace, workspace_bytes, s));
   const Val& in = p->val[0];
   const long n = (long)in.C * in.hw();
   float* nrm = norms ? norms : p->at(p->off_norms);
   float* v = p->at(p->off_v);
-  TRY(ganamd_gp_fwd(g, p->B, n, center, lambda, mode, nrm, penalty, p->at(p->off_gp), s));
+  TRY(ganamd_gp_fwd(g, p->B, n, center, lambda, mode, nrm, penalty, p->at(p->off_gp), p->gp_ws, s));
   // gout = 1: the ones the backward's seed left at off_ones (B >= 1 of them)
   TRY(ganamd_gp_bwd(g, nrm, p->at(p->off_ones), p->B, n, center, lambda, mode, v, s));
-  TRY(ganamd_critic_tangent(p, v, gr, workspace, s));
-  return ganamd_critic_adjoint(p, nullptr, gr, nullptr, workspace, s);
+  TRY(ganamd_critic_tangent(p, v, gr, workspace, workspace_bytes, s));
+  return ganamd_critic_adjoint(p, nullptr, gr, nullptr, workspace, workspace_bytes, s);
 }
 
 }  // extern "C"

@@ -69,9 +69,11 @@ extern "C" size_t ganamd_image_batch_workspace(int B, int H, int OW) { return (s
 
 extern "C" int ganamd_image_batch(const uint8_t* src, int B, int H, int W, const uint8_t* flip, const int32_t* ix,
                                   const float* wx, int KX, int OW, const int32_t* iy, const float* wy, int KY, int OH,
-                                  const float* mean, const float* stdv, float* y, float* ws, hipStream_t stream) {
+                                  const float* mean, const float* stdv, float* y, float* ws, size_t ws_bytes,
+                                  hipStream_t stream) {
   if (!src || !ix || !wx || !iy || !wy || !mean || !stdv || !y || !ws) return GANAMD_EINVAL;
   if (B <= 0 || H <= 0 || W <= 0 || KX <= 0 || KY <= 0 || OW <= 0 || OH <= 0) return GANAMD_EINVAL;
+  if (ws_bytes < ganamd_image_batch_workspace(B, H, OW)) return GANAMD_EINVAL;
   const long n1 = (long)B * 3 * H * OW, n2 = (long)B * 3 * OH * OW;
   img_rows_kernel<<<grid_for(n1), 256, 0, stream>>>(src, B, H, W, flip, ix, wx, KX, OW, ws);
   img_cols_kernel<<<grid_for(n2), 256, 0, stream>>>(ws, B, H, OW, iy, wy, KY, OH, mean, stdv, y);

@@ -965,9 +965,9 @@ size_t ganamd_rowreduce_workspace(int C, long L) {
 int ganamd_bn_act_fwd_seg(const float* x, int C, long L, int seg, const float* gamma, const float* beta,
                           const float* alpha, float* running_mean, float* running_var, float momentum, float eps,
                           float* y, float* save_mean, float* save_invstd, float* seg_uvar, void* workspace,
-                          hipStream_t st) {
+                          size_t workspace_bytes, hipStream_t st) {
   if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || C <= 0 || L <= 0 || seg < 1 ||
-      L % seg || (seg > 1 && !seg_uvar))
+      L % seg || (seg > 1 && !seg_uvar) || workspace_bytes < ganamd_rowreduce_workspace(C * seg, L / seg))
     return GANAMD_EINVAL;
   // rows of the segmented problem: (channel, segment), each L / seg long; the parameters of row r
   // are channel r / seg's, the running statistics are updated per segment in order afterwards
@@ -997,15 +997,17 @@ int ganamd_bn_act_fwd_seg(const float* x, int C, long L, int seg, const float* g
 
 int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
-                      float* save_mean, float* save_invstd, void* workspace, hipStream_t st) {
+                      float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes, hipStream_t st) {
   return ganamd_bn_act_fwd_seg(x, C, L, 1, gamma, beta, alpha, running_mean, running_var, momentum, eps, y, save_mean,
-                               save_invstd, nullptr, workspace, st);
+                               save_invstd, nullptr, workspace, workspace_bytes, st);
 }
 
 int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,
                       const float* alpha, const float* save_mean, const float* save_invstd, float* gx, float* ggamma,
-                      float* gbeta, float* galpha, int accumulate, void* workspace, hipStream_t st) {
-  if (!gy || !x || !gamma || !beta || !save_mean || !save_invstd || !gx || !ggamma || !gbeta || !workspace)
+                      float* gbeta, float* galpha, int accumulate, void* workspace, size_t workspace_bytes,
+                      hipStream_t st) {
+  if (!gy || !x || !gamma || !beta || !save_mean || !save_invstd || !gx || !ggamma || !gbeta || !workspace ||
+      C <= 0 || L <= 0 || workspace_bytes < ganamd_rowreduce_workspace(C, L))
     return GANAMD_EINVAL;
   if (L <= kSmallL) {
     hipLaunchKernelGGL(bn_small_bwd_kernel, dim3((C + 3) / 4), dim3(kNT), 0, st, gy, x, C, (int)L, save_mean,
@@ -1038,8 +1040,10 @@ int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y
 }
 
 int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C, long L, float* gx, float* galpha,
-                     int accumulate, void* workspace, hipStream_t st) {
-  if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
+                     int accumulate, void* workspace, size_t workspace_bytes, hipStream_t st) {
+  if (!gy || !x || !alpha || C <= 0 || L <= 0 ||
+      (galpha && (!workspace || workspace_bytes < ganamd_rowreduce_workspace(C, L))))
+    return GANAMD_EINVAL;
   const int S = splits_for(L);
   float* part = galpha ? (S == 1 ? galpha : static_cast<float*>(workspace)) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, gy, x, alpha, L, S, gx, part,
@@ -1050,8 +1054,11 @@ int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C,
 }
 
 int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy, const float* x, const float* alpha,
-                         int C, long L, float* ggy, float* gx, float* galpha, void* workspace, hipStream_t st) {
-  if (!gy || !x || !alpha || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
+                         int C, long L, float* ggy, float* gx, float* galpha, void* workspace,
+                         size_t workspace_bytes, hipStream_t st) {
+  if (!gy || !x || !alpha || C <= 0 || L <= 0 ||
+      (galpha && (!workspace || workspace_bytes < ganamd_rowreduce_workspace(C, L))))
+    return GANAMD_EINVAL;
   const int S = splits_for(L);
   float* part = galpha ? (S == 1 ? galpha : static_cast<float*>(workspace)) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, ggx, ggalpha, gy, x, alpha, L, S, ggy, gx,
@@ -1062,8 +1069,10 @@ int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy
 }
 
 int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const float* alpha, int C, long L, float* yd,
-                         float* galpha, int accumulate, void* workspace, hipStream_t st) {
-  if (!xd || !gy || !x || !alpha || !yd || C <= 0 || L <= 0 || (galpha && !workspace)) return GANAMD_EINVAL;
+                         float* galpha, int accumulate, void* workspace, size_t workspace_bytes, hipStream_t st) {
+  if (!xd || !gy || !x || !alpha || !yd || C <= 0 || L <= 0 ||
+      (galpha && (!workspace || workspace_bytes < ganamd_rowreduce_workspace(C, L))))
+    return GANAMD_EINVAL;
   const int S = splits_for(L);
   float* part = galpha ? (S == 1 ? galpha : static_cast<float*>(workspace)) : nullptr;
   hipLaunchKernelGGL(prelu_bwd_bwd_kernel, dim3(S, C), dim3(kNT), 0, st, xd, nullptr, gy, x, alpha, L, S, yd, nullptr,
@@ -1127,8 +1136,9 @@ int ganamd_modconv_sd_bwd(const float* gy, const float* y, const float* noise, c
 }
 
 int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, int accumulate, void* workspace,
-                   hipStream_t st) {
-  if (!a || !out || !workspace || C <= 0 || L <= 0) return GANAMD_EINVAL;
+                   size_t workspace_bytes, hipStream_t st) {
+  if (!a || !out || !workspace || C <= 0 || L <= 0 || workspace_bytes < ganamd_rowreduce_workspace(C, L))
+    return GANAMD_EINVAL;
   const int S = splits_for(L);
   if (S == 1) {
     hipLaunchKernelGGL(row_dot_kernel, dim3(S, C), dim3(kNT), 0, st, a, b, L, S, out, 1 + (accumulate != 0));

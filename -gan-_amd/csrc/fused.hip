@@ -302,8 +302,10 @@ size_t ganamd_gp_workspace(int B, long n) {
 }
 
 int ganamd_gp_fwd(const float* g, int B, long n, float center, float lambda, int mode, float* norms, float* out,
-                  void* workspace, hipStream_t st) {
-  if (!g || !norms || !out || !workspace || B <= 0 || n <= 0 || (mode != 0 && mode != 1)) return GANAMD_EINVAL;
+                  void* workspace, size_t workspace_bytes, hipStream_t st) {
+  if (!g || !norms || !out || !workspace || B <= 0 || n <= 0 || (mode != 0 && mode != 1) ||
+      workspace_bytes < ganamd_gp_workspace(B, n))
+    return GANAMD_EINVAL;
   const int S = (int)std::min<long>(64, std::max<long>(1, (n + kGpChunk - 1) / kGpChunk));
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(gp_partial_kernel, dim3(S, B), dim3(kNT), 0, st, g, n, S, part);

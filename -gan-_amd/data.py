@@ -18,6 +18,7 @@ import torch
 
 from . import tables
 from ._lib import LIB, check, ptr, stream, workspace
+from ._lib import ws as wsarg
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)   # units/dataloader.py:12
 IMAGENET_STD = (0.229, 0.224, 0.225)
@@ -59,7 +60,7 @@ class ImagePipeline:
         ws = workspace(LIB.ganamd_image_batch_workspace(B, H, self.size), images.device)
         check(LIB.ganamd_image_batch(images.data_ptr(), B, H, W, flip.data_ptr(), ix.data_ptr(), ptr(wx), kx,
                                      self.size, iy.data_ptr(), ptr(wy), ky, self.size, ptr(self.mean), ptr(self.std),
-                                     ptr(y), ptr(ws), stream()), "image_batch")
+                                     ptr(y), *wsarg(ws), stream()), "image_batch")
         return y
 
 

@@ -25,6 +25,7 @@ from torch.autograd.graph import get_gradient_edge
 
 from . import _lib
 from ._lib import LIB, check, iptr, ptr, stream, workspace
+from ._lib import ws as wsarg
 from . import tables
 
 # ------------------------------------------------------------------------------------------
@@ -48,16 +49,17 @@ class Geo:
     transposed: bool = False
 
     def desc(self, packed=False):
-        key = (self, packed, _MATH[0])
+        key = (self, packed, _MATH[0], _KOFF[0])
         d = _DESC_CACHE.get(key)
         if d is None:
             d = _lib.ConvDesc(self.B, self.Cin, self.H, self.W, self.Cout, self.OH, self.OW, self.K, self.K,
-                              self.stride, self.pad, self.pad_mode, int(self.transposed), int(packed), _MATH[0])
+                              self.stride, self.pad, self.pad_mode, int(self.transposed), int(packed), _MATH[0],
+                              _KOFF[0])
             _DESC_CACHE[key] = d
         return d
 
     def ws_bytes(self, op, packed=False):
-        key = (self, op, packed, _MATH[0])
+        key = (self, op, packed, _MATH[0], _KOFF[0])
         v = _WS_CACHE.get(key)
         if v is None:
             n = _lib.c_size_t(0)
@@ -73,6 +75,7 @@ class Geo:
 _DESC_CACHE: dict = {}
 _WS_CACHE: dict = {}
 _MATH = [_lib.MATH_F32]      # arithmetic of the conv GEMMs launched now (math_mode)
+_KOFF = [0]                  # ganamd_conv_desc.kernel_off of the convs launched now (patch_conv)
 
 
 @contextlib.contextmanager
@@ -91,16 +94,26 @@ def math_mode(mode: str):
 PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus", "kernel")
 
 
+def set_patch(mask: int = 7) -> int:
+    """Which stride-1 convs this process's layers send to the split6 LDS-patch kernels (bit 0
+    forward, bit 1 dgrad, bit 2 the row-blocked weight gradient; default 7 = all; 0 = the gather
+    GEMMs, for A/B and tests).  It only sets the ``kernel_off`` field of the descriptors this module
+    builds (and of critic plans created afterwards): the library itself keeps no such state.  Like
+    ``math_mode`` it is read by the backward too (autograd runs it on its own threads), so it is
+    process-wide for the Python layers.  Returns the previous mask."""
+    prev = (~_KOFF[0]) & 7
+    _KOFF[0] = (~int(mask)) & 7
+    return prev
+
+
 @contextlib.contextmanager
 def patch_conv(mask: int = 7):
-    """Which stride-1 convs take the split6 LDS-patch kernels inside the block (bit 0 forward, bit 1
-    dgrad, bit 2 the row-blocked weight gradient; ganamd_conv_set_patch, library default 7 = all):
-    mask 0 runs the gather GEMMs instead (A/B, tests)."""
-    prev = LIB.ganamd_conv_set_patch(int(mask))
+    """``set_patch(mask)`` inside the block."""
+    prev = set_patch(mask)
     try:
         yield
     finally:
-        LIB.ganamd_conv_set_patch(prev)
+        set_patch(prev)
 
 
 def plan_info(geo: "Geo", op: int, scaled: bool = False) -> dict:
@@ -339,7 +352,7 @@ def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0, out=None):
     nb = geo.ws_bytes(_lib.CONV_FWD, packed)
     ws = workspace(nb, x.device) if nb else None
     check(LIB.ganamd_conv_fwd(geo.desc(packed), ptr(x), ptr(pw if packed else w), ptr(bias), ptr(xs), ptr(ys),
-                              float(alpha), ptr(y), ptr(ws), stream()), "conv_fwd")
+                              float(alpha), ptr(y), *wsarg(ws), stream()), "conv_fwd")
     return y
 
 
@@ -354,7 +367,7 @@ def _conv_dgrad(geo: Geo, gy, w, gys=None, alpha=1.0):
     nb = geo.ws_bytes(_lib.CONV_DGRAD, packed)
     ws = workspace(nb, gy.device) if nb else None
     check(LIB.ganamd_conv_dgrad(geo.desc(packed), ptr(gy), ptr(pw if packed else w), ptr(gys), float(alpha), ptr(gx),
-                                ptr(ws), stream()), "conv_dgrad")
+                                *wsarg(ws), stream()), "conv_dgrad")
     return gx
 
 
@@ -370,7 +383,7 @@ def _conv_wgrad(geo: Geo, x, gy, xs=None, gys=None, alpha=1.0, out=None, accumul
     nb = geo.ws_bytes(_lib.CONV_WGRAD)
     ws = workspace(nb, x.device) if nb else None
     check(LIB.ganamd_conv_wgrad(geo.desc(), ptr(x), ptr(gy), ptr(xs), ptr(gys), float(alpha), ptr(gw),
-                                int(accumulate), ptr(ws), stream()), "conv_wgrad")
+                                int(accumulate), *wsarg(ws), stream()), "conv_wgrad")
     return gw
 
 
@@ -415,7 +428,7 @@ def row_sum_acc(a, out):
     C, L = _rows(a)
     _need(out, C, "row_sum out")
     ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), a.device)
-    check(LIB.ganamd_row_dot(ptr(a), None, C, L, ptr(out), 1, ptr(ws), stream()), "row_dot")
+    check(LIB.ganamd_row_dot(ptr(a), None, C, L, ptr(out), 1, *wsarg(ws), stream()), "row_dot")
 
 
 class ConvFwd(Function):
@@ -544,7 +557,7 @@ class PReLU(Function):
             C, L = _rows(x)
             gx = torch.empty_like(x)
             ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
-            check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(x), ptr(a), C, L, ptr(gx), ptr(tgt), 1, ptr(ws), stream()),
+            check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(x), ptr(a), C, L, ptr(gx), ptr(tgt), 1, *wsarg(ws), stream()),
                   "prelu_bwd")
             return gx, None
         av = ctx.a_arg if ctx.a_arg.is_contiguous() else a
@@ -563,7 +576,7 @@ class PReLUBackward(Function):
         gx = torch.empty_like(x)
         ga = torch.empty_like(a)
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
-        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), ptr(ga), 0, ptr(ws), stream()),
+        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), ptr(ga), 0, *wsarg(ws), stream()),
               "prelu_bwd")
         ctx.save_for_backward(gy, x, a)
         return gx, ga
@@ -584,7 +597,7 @@ class PReLUBackward(Function):
             return None, None, None
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
         check(LIB.ganamd_prelu_bwd_bwd(ptr(ggx), ptr(gga), ptr(gy), ptr(x), ptr(a), C, L, ptr(g_gy), ptr(g_x),
-                                       ptr(g_a), ptr(ws), stream()), "prelu_bwd_bwd")
+                                       ptr(g_a), *wsarg(ws), stream()), "prelu_bwd_bwd")
         if tgt is not None:
             tgt.add_(g_a)          # one tiny add; the kernel has no accumulate form
             g_a = None
@@ -617,7 +630,7 @@ class PReLUBackwardX(Function):
             tgt = flat_grad(ctx.a_arg)
             ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
             check(LIB.ganamd_prelu_bwd_bwd(ptr(_c(ggx)), None, ptr(gy), ptr(x), ptr(a), C, L, None, None, ptr(g_a),
-                                           ptr(ws), stream()), "prelu_bwd_bwd")
+                                           *wsarg(ws), stream()), "prelu_bwd_bwd")
             if tgt is not None:
                 tgt.add_(g_a)
                 g_a = None
@@ -649,7 +662,7 @@ class BNAct(Function):
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
         check(LIB.ganamd_bn_act_fwd(ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(running_mean),
                                     ptr(running_var), float(momentum), float(eps), ptr(y), ptr(mean), ptr(invstd),
-                                    ptr(ws), stream()), "bn_act_fwd")
+                                    *wsarg(ws), stream()), "bn_act_fwd")
         ctx.save_for_backward(x, gamma, beta, alpha, mean, invstd)
         ctx.has_alpha = alpha is not None
         ctx.args = (gamma, beta, alpha)
@@ -674,7 +687,7 @@ class BNAct(Function):
             ga = torch.empty_like(alpha) if ctx.has_alpha else None
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
         check(LIB.ganamd_bn_act_bwd(ptr(gy), ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(mean), ptr(invstd),
-                                    ptr(gx), ptr(gg), ptr(gb), ptr(ga), int(direct), ptr(ws), stream()), "bn_act_bwd")
+                                    ptr(gx), ptr(gg), ptr(gb), ptr(ga), int(direct), *wsarg(ws), stream()), "bn_act_bwd")
         if direct:
             return gx, None, None, None, None, None, None, None
         return gx, gg, gb, ga, None, None, None, None
@@ -711,7 +724,7 @@ def bn_fwd_raw(x, C, L, gamma, beta, alpha, running_mean, running_var, momentum,
     ws = workspace(LIB.ganamd_rowreduce_workspace(C * seg, L // seg), x.device)
     check(LIB.ganamd_bn_act_fwd_seg(ptr(x), C, L, seg, ptr(gamma), ptr(beta), ptr(alpha), ptr(running_mean),
                                     ptr(running_var), float(momentum), float(eps), ptr(y), ptr(mean), ptr(invstd),
-                                    ptr(uvar), ptr(ws), stream()), "bn_act_fwd_seg")
+                                    ptr(uvar), *wsarg(ws), stream()), "bn_act_fwd_seg")
     return y, mean, invstd
 
 
@@ -744,7 +757,7 @@ def linear_bn_act(x, w, bias, alpha: float, bn, act=None):
     check(LIB.ganamd_linear_bn_act(geo.desc(packed), ptr(x), ptr(pw if packed else wv), ptr(bias), float(alpha),
                                    ptr(bn.weight), ptr(bn.bias), ptr(None if act is None else act.weight),
                                    ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum), float(bn.eps),
-                                   ptr(y), ptr(ws), stream()), "linear_bn_act")
+                                   ptr(y), *wsarg(ws), stream()), "linear_bn_act")
     return y
 
 
@@ -1024,7 +1037,7 @@ class GradPenalty(Function):
         norms = torch.empty(B, device=g.device, dtype=torch.float32)
         out = torch.empty((), device=g.device, dtype=torch.float32)
         ws = workspace(LIB.ganamd_gp_workspace(B, n), g.device)
-        check(LIB.ganamd_gp_fwd(ptr(g), B, n, float(center), float(lam), int(mode), ptr(norms), ptr(out), ptr(ws),
+        check(LIB.ganamd_gp_fwd(ptr(g), B, n, float(center), float(lam), int(mode), ptr(norms), ptr(out), *wsarg(ws),
                                 stream()), "gp_fwd")
         ctx.save_for_backward(g, norms)
         ctx.args = (B, n, float(center), float(lam), int(mode))
@@ -1180,7 +1193,7 @@ class AddPReLU(Function):
         ga = tgt if tgt is not None else torch.empty_like(alpha)
         ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), z.device)
         check(LIB.ganamd_prelu_bwd(ptr(_c(gy)), ptr(z), ptr(alpha), C, L, ptr(gz), ptr(ga), int(tgt is not None),
-                                   ptr(ws), stream()), "prelu_bwd")
+                                   *wsarg(ws), stream()), "prelu_bwd")
         return gz, gz, (None if tgt is not None else ga)
 
 
@@ -1254,7 +1267,7 @@ def _conv_fwd_ex(geo, x, w, xs, ys, alpha, noise=None, noise_scale=None, act=Non
     ws = workspace(nb, x.device) if nb else None
     check(LIB.ganamd_conv_fwd_ex(geo.desc(packed), ptr(x), ptr(pw if packed else _c(w)), None, ptr(xs), ptr(ys),
                                  float(alpha), ptr(None if noise is None else _c(noise)), ptr(noise_scale),
-                                 ptr(act), ptr(y), ptr(ws), stream()), "conv_fwd_ex")
+                                 ptr(act), ptr(y), *wsarg(ws), stream()), "conv_fwd_ex")
     return y
 
 

@@ -57,25 +57,30 @@ typedef struct ganamd_conv_desc {
   int32_t packed_w;   /* 1: the w argument of conv_fwd/conv_dgrad is already in GEMM order
                          (ganamd_conv_pack for the same op and geometry); 0: as stored */
   int32_t math;       /* GANAMD_MATH_F32 | GANAMD_MATH_BF16 */
+  int32_t kernel_off; /* kernels this call must NOT use (0 = the library's choice, all allowed):
+                         GANAMD_KERNEL_PATCH_FWD / _PATCH_DGRAD (the split6 LDS-patch conv of
+                         stride-1 3x3 / 5x5 convs on 32- / 64-wide maps, csrc/conv_patch.hip) and
+                         GANAMD_KERNEL_WGRAD_ROW (the row-blocked weight gradient,
+                         csrc/conv_wgrad_row.hip) -- a per-call A/B switch, no library state */
 } ganamd_conv_desc;
 
-/* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD). */
+#define GANAMD_KERNEL_PATCH_FWD 1
+#define GANAMD_KERNEL_PATCH_DGRAD 2
+#define GANAMD_KERNEL_WGRAD_ROW 4
+
+/* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD).  Every entry point that takes a
+ * workspace also takes its size in bytes and returns GANAMD_EINVAL (launching nothing) when it is
+ * smaller than this query's answer for the same descriptor. */
 int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes);
 
-/* The block schedule conv_fwd / conv_dgrad will launch (introspection for tests and tools):
+/* The block schedule conv_fwd / conv_dgrad will launch for d (d->kernel_off included;
+ * introspection for tests and tools):
  * info[11] = {BM, BN, column tiles, row tiles, whole-tile columns, tail K-splits, K-steps per
  * split, blocks launched, resident blocks per CU of the instance, CUs, kernel (0: the gather
  * GEMM, 1: the split6 LDS-patch conv -- BN is then its pixel region: 512 pixels at W = 64,
  * 256 at W = 32)}.  scaled: whether the x_scale / gy_scale operand will be passed (it selects
  * the kernel instance). */
 int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* info);
-/* Which stride-1 "same" convolutions on 32- / 64-wide maps take the split6 LDS-patch kernel
- * (csrc/conv_patch.hip) where its domain and grid fit: bit 0 forward, bit 1 dgrad interior, bit 2
- * the row-blocked weight gradient (csrc/conv_wgrad_row.hip) (default 7 = all; 0 = the gather GEMMs
- * everywhere, for A/B).  mask < 0 only queries.  Returns
- * the previous mask.  Plans are chosen at launch (or graph capture) time; the packed-weight
- * layout does not depend on the mask. */
-int ganamd_conv_set_patch(int mask);
 
 /* The weight operand of conv_fwd / conv_dgrad in GEMM order (rows padded to the tile grid,
  * channels to whole K-steps, zero filled).  A caller that reuses a weight across calls (the
@@ -113,7 +118,7 @@ int ganamd_conv_pack_batch(const ganamd_pack_job* jobs, int n_jobs, int64_t tota
  * (split-K partial tiles when the output grid is too small to fill the chip; may be 0). */
 int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                     const float* x_scale, const float* y_scale, float alpha, float* y, void* workspace,
-                    hipStream_t stream);
+                    size_t workspace_bytes, hipStream_t stream);
 
 /* ganamd_conv_fwd with an extended epilogue, applied after bias in this order:
  *   y += noise_scale[co] * noise[co][b,oh,ow]      (StyleConv noise, generator_13_5.py:263-266)
@@ -123,27 +128,28 @@ int ganamd_conv_fwd(const ganamd_conv_desc* d, const float* x, const float* w, c
 int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias,
                        const float* x_scale, const float* y_scale, float alpha, const float* noise,
                        const float* noise_scale, const float* act_alpha, float* y, void* workspace,
-                       hipStream_t stream);
+                       size_t workspace_bytes, hipStream_t stream);
 
 /* gx = alpha * dConv/dx applied to (gy * gy_scale[co][b]), including the ReplicationPad2d
  * backward (edge folding).  Replaces aten convolution_backward (input grad) + replication_pad2d_backward.
  * Workspace: ganamd_conv_workspace(d, GANAMD_CONV_DGRAD). */
 int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w, const float* gy_scale,
-                      float alpha, float* gx, void* workspace, hipStream_t stream);
+                      float alpha, float* gx, void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* gw (+)= alpha * dConv/dW for inputs (x * x_scale) and (gy * gy_scale) (both scales or
  * neither).  accumulate=0 overwrites gw.  Replaces aten convolution_backward (weight grad).
  * Workspace: ganamd_conv_workspace(d, GANAMD_CONV_WGRAD).  Deterministic (no atomics). */
 int ganamd_conv_wgrad(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x_scale,
                       const float* gy_scale, float alpha, float* gw, int accumulate, void* workspace,
-                      hipStream_t stream);
+                      size_t workspace_bytes, hipStream_t stream);
 
 /* gw (+)= alpha * [dConv/dW(x, gy) + dConv/dW(x2, gy2)] as ONE GEMM over both pixel ranges (two
  * K segments of the same weight gradient; unscaled, not transposed, else two launches).  The critic
  * adjoint's x * a + xd * g (critic.hip; the second-order term of the gradient penalty,
  * train/wgangp.py:68-69).  Workspace: ganamd_conv_workspace(d, GANAMD_CONV_WGRAD). */
 int ganamd_conv_wgrad2(const ganamd_conv_desc* d, const float* x, const float* gy, const float* x2, const float* gy2,
-                       float alpha, float* gw, int accumulate, void* workspace, hipStream_t stream);
+                       float alpha, float* gw, int accumulate, void* workspace, size_t workspace_bytes,
+                       hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Train-mode BatchNorm (1d or 2d) fused with an optional per-channel PReLU.
@@ -156,7 +162,8 @@ size_t ganamd_rowreduce_workspace(int C, long L);
 
 int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const float* beta, const float* alpha,
                       float* running_mean, float* running_var, float momentum, float eps, float* y,
-                      float* save_mean, float* save_invstd, void* workspace, hipStream_t stream);
+                      float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
+                      hipStream_t stream);
 /* Segmented form: x holds `seg` independent mini-batches stacked along the batch (each row's L
  * elements are seg consecutive runs of L / seg), each normalised with its OWN statistics -- the
  * outputs of seg separate calls, in one launch (the critic steps' fake batches generated in one
@@ -166,7 +173,7 @@ int ganamd_bn_act_fwd(const float* x, int C, long L, const float* gamma, const f
 int ganamd_bn_act_fwd_seg(const float* x, int C, long L, int seg, const float* gamma, const float* beta,
                           const float* alpha, float* running_mean, float* running_var, float momentum, float eps,
                           float* y, float* save_mean, float* save_invstd, float* seg_uvar, void* workspace,
-                          hipStream_t stream);
+                          size_t workspace_bytes, hipStream_t stream);
 
 /* Backward of ganamd_bn_act_fwd: writes gx [C][L]; ggamma, gbeta, galpha ([C]; galpha may be
  * NULL when alpha is NULL) are overwritten, or accumulated into when accumulate = 1 (parameter
@@ -174,7 +181,7 @@ int ganamd_bn_act_fwd_seg(const float* x, int C, long L, int seg, const float* g
 int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const float* gamma, const float* beta,
                       const float* alpha, const float* save_mean, const float* save_invstd, float* gx,
                       float* ggamma, float* gbeta, float* galpha, int accumulate, void* workspace,
-                      hipStream_t stream);
+                      size_t workspace_bytes, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * PReLU (per-channel slope) with first and second derivatives (nn.PReLU; the critic's
@@ -183,18 +190,20 @@ int ganamd_bn_act_bwd(const float* gy, const float* x, int C, long L, const floa
 int ganamd_prelu_fwd(const float* x, const float* alpha, int C, long L, float* y, hipStream_t stream);
 /* gx = gy * (x>0 ? 1 : alpha); galpha[c] (=|+= with accumulate) sum gy*x over x<=0 */
 int ganamd_prelu_bwd(const float* gy, const float* x, const float* alpha, int C, long L, float* gx, float* galpha,
-                     int accumulate, void* workspace, hipStream_t stream);
+                     int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream);
 /* Backward of ganamd_prelu_bwd given ggx = dR/dgx and ggalpha = dR/dgalpha (may be NULL):
  *   ggy = ggx*(x>0?1:alpha) + ggalpha[c]*(x>0?0:x)
  *   gx  = ggalpha[c]*gy*(x>0?0:1)            (may be NULL)
  *   galpha[c] = sum ggx*gy over x<=0         (may be NULL) */
 int ganamd_prelu_bwd_bwd(const float* ggx, const float* ggalpha, const float* gy, const float* x, const float* alpha,
-                         int C, long L, float* ggy, float* gx, float* galpha, void* workspace, hipStream_t stream);
+                         int C, long L, float* ggy, float* gx, float* galpha, void* workspace,
+                         size_t workspace_bytes, hipStream_t stream);
 /* Tangent sweep of the critic's gradient-penalty double backward (critic.py) through a PReLU:
  *   yd = xd * (x>0 ? 1 : alpha);  galpha[c] (=|+= with accumulate) sum gy*xd over x<=0
  * (the slope's second-order term; gy = the first backward's gradient at the PReLU output). */
-int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const float* alpha, int C, long L, float* yd,
-                         float* galpha, int accumulate, void* workspace, hipStream_t stream);
+int ganamd_prelu_tangent(const float* xd, const float* gy, const float* x, const float* alpha, int C, long L,
+                         float* yd,
+                         float* galpha, int accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Separable 2-D resampling with per-axis tap tables (ELL format, K taps per output index):
@@ -242,7 +251,7 @@ int ganamd_modconv_sd_bwd(const float* gy, const float* y, const float* noise, c
 /* out[c] (=|+= with accumulate) sum_{l} a[c][l] * (b ? b[c][l] : 1) over rows of length L
  * (with b = NULL and accumulate = 1: a conv bias gradient added into the flat gradient buffer). */
 int ganamd_row_dot(const float* a, const float* b, int C, long L, float* out, int accumulate, void* workspace,
-                   hipStream_t stream);
+                   size_t workspace_bytes, hipStream_t stream);
 
 /* out[i] = sum_{t<T} w[i*T + t]^2  (row sums of squares; the demodulation norm's sum over taps) */
 int ganamd_segment_sumsq(const float* w, long rows, int T, float* out, hipStream_t stream);
@@ -312,7 +321,7 @@ int ganamd_route_bwd(int n, const float* const* g, const int32_t* lo, const int3
  * graph of the penalty itself.  Workspace: ganamd_gp_workspace(B, n) bytes. */
 size_t ganamd_gp_workspace(int B, long n);
 int ganamd_gp_fwd(const float* g, int B, long n, float center, float lambda, int mode, float* norms, float* out,
-                  void* workspace, hipStream_t stream);
+                  void* workspace, size_t workspace_bytes, hipStream_t stream);
 int ganamd_gp_bwd(const float* g, const float* norms, const float* gout, int B, long n, float center, float lambda,
                   int mode, float* dg, hipStream_t stream);
 
@@ -327,7 +336,8 @@ int ganamd_gp_bwd(const float* g, const float* norms, const float* gout, int B, 
 size_t ganamd_image_batch_workspace(int B, int H, int OW);
 int ganamd_image_batch(const uint8_t* src, int B, int H, int W, const uint8_t* flip, const int32_t* ix,
                        const float* wx, int KX, int OW, const int32_t* iy, const float* wy, int KY, int OH,
-                       const float* mean, const float* stdv, float* y, float* workspace, hipStream_t stream);
+                       const float* mean, const float* stdv, float* y, float* workspace, size_t workspace_bytes,
+                       hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Pointwise activations (csrc/act.hip) over n contiguous floats.
@@ -345,7 +355,8 @@ int ganamd_act_fwd(int kind, const float* x, long n, float slope, float* y, hipS
 int ganamd_act_bwd(int kind, const float* v, const float* gy, long n, float slope, float* gx, hipStream_t stream);
 /* Adjoint sweep of the critic's gradient-penalty double backward (critic.py) through an
  * activation: ax = ay * f'(.) + gy * xd * f''(.)  (v as for ganamd_act_bwd; f'' = 0 for leaky). */
-int ganamd_act_adjoint(int kind, const float* v, const float* ay, const float* gy, const float* xd, long n, float slope,
+int ganamd_act_adjoint(int kind, const float* v, const float* ay, const float* gy, const float* xd, long n,
+                       float slope,
                        float* ax, hipStream_t stream);
 
 /* y = x1 * s1[plane] + x2 * s2[plane] + r over planes of HW floats (x2/s2 and r may be NULL): the
@@ -382,13 +393,14 @@ int ganamd_softmax_m_bwd(int M, const float* y, const float* gy, long P, float* 
  * ------------------------------------------------------------------------------------- */
 size_t ganamd_mbstd_workspace(int S);
 int ganamd_mbstd_fwd(const float* x, long ldx, int C, int B, int HW, int S, int G, float* y, long ldy, float* std_out,
-                     void* workspace, hipStream_t stream);
+                     void* workspace, size_t workspace_bytes, hipStream_t stream);
 int ganamd_mbstd_bwd(const float* x, long ldx, const float* gy, long ldy, int C, int B, int HW, int S, int G,
-                     float* gx, void* workspace, hipStream_t stream);
+                     float* gx, void* workspace, size_t workspace_bytes, hipStream_t stream);
 int ganamd_mbstd_tangent(const float* x, const float* xd, long ldx, int C, int B, int HW, int S, int G, float* yd,
-                         long ldy, void* workspace, hipStream_t stream);
+                         long ldy, void* workspace, size_t workspace_bytes, hipStream_t stream);
 int ganamd_mbstd_adjoint(const float* x, const float* xd, long ldx, const float* gy, const float* ay, long ldy, int C,
-                         int B, int HW, int S, int G, float* ax, void* workspace, hipStream_t stream);
+                         int B, int HW, int S, int G, float* ax, void* workspace, size_t workspace_bytes,
+                         hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Linear + train-mode BatchNorm1d (+ PReLU) in one launch, the generator's
@@ -403,7 +415,7 @@ int ganamd_mbstd_adjoint(const float* x, const float* xd, long ldx, const float*
 int ganamd_linear_bn_act(const ganamd_conv_desc* d, const float* x, const float* w, const float* bias, float alpha,
                          const float* gamma, const float* beta, const float* act_alpha, float* running_mean,
                          float* running_var, float momentum, float eps, float* y, void* workspace,
-                         hipStream_t stream);
+                         size_t workspace_bytes, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Device random numbers (Philox4x32-10) for z, eps and the StyleConv noise.
@@ -519,9 +531,10 @@ typedef struct ganamd_critic_grads {
 typedef struct ganamd_critic_plan ganamd_critic_plan;
 
 /* Validates the program and sizes every value; NULL on an invalid program (shape mismatch,
- * unknown op, a value used before it is defined).  math: GANAMD_MATH_F32 | GANAMD_MATH_BF16. */
+ * unknown op, a value used before it is defined).  math: GANAMD_MATH_F32 | GANAMD_MATH_BF16;
+ * kernel_off: the ganamd_conv_desc.kernel_off of every conv the plan issues (0: all kernels). */
 ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops, int B, int C0, int H0, int W0,
-                                         int segments, int math);
+                                         int segments, int math, int kernel_off);
 void ganamd_critic_destroy(ganamd_critic_plan* plan);
 int ganamd_critic_workspace(const ganamd_critic_plan* plan, size_t* bytes);
 /* The workspace in four regions, each allocated only when the sweep that fills it starts:
@@ -529,22 +542,24 @@ int ganamd_critic_workspace(const ganamd_critic_plan* plan, size_t* bytes);
  * `workspace` = NULL every sweep uses the regions bound here (binding region 0 starts a new
  * evaluation); with a non-NULL `workspace` (ganamd_critic_workspace bytes) the four regions are
  * carved from it in that order.  A first-order evaluation (the real / fake critic passes) then
- * needs regions 0-1 only. */
+ * needs regions 0-1 only.  Bound regions and the contiguous workspace carry their byte sizes
+ * (region_bytes / workspace_bytes), checked against these queries: GANAMD_EINVAL when short. */
 int ganamd_critic_region_bytes(const ganamd_critic_plan* plan, int which, size_t* bytes);
-int ganamd_critic_bind(ganamd_critic_plan* plan, int which, void* region);
+int ganamd_critic_bind(ganamd_critic_plan* plan, int which, void* region, size_t region_bytes);
 /* Device pointer of value v in sweep `which` (0 X, 1 G, 2 XD, 3 A) as the last sweep left it
  * (NULL: no such value yet).  For callers that read saved activations / gradients. */
 int ganamd_critic_value(const ganamd_critic_plan* plan, int which, int v, const float** ptr);
-int ganamd_critic_forward(ganamd_critic_plan* plan, const float* x, float* out, void* workspace, hipStream_t stream);
+int ganamd_critic_forward(ganamd_critic_plan* plan, const float* x, float* out, void* workspace,
+                          size_t workspace_bytes, hipStream_t stream);
 int ganamd_critic_backward(ganamd_critic_plan* plan, const float* seed, const ganamd_critic_grads* grads, float* gx,
-                           void* workspace, hipStream_t stream);
-int ganamd_critic_tangent(ganamd_critic_plan* plan, const float* v, const ganamd_critic_grads* grads, void* workspace,
-                          hipStream_t stream);
+                           void* workspace, size_t workspace_bytes, hipStream_t stream);
+int ganamd_critic_tangent(ganamd_critic_plan* plan, const float* v, const ganamd_critic_grads* grads,
+                          void* workspace, size_t workspace_bytes, hipStream_t stream);
 int ganamd_critic_adjoint(ganamd_critic_plan* plan, const float* a_seed, const ganamd_critic_grads* grads, float* ax,
-                          void* workspace, hipStream_t stream);
+                          void* workspace, size_t workspace_bytes, hipStream_t stream);
 int ganamd_critic_gp_step(ganamd_critic_plan* plan, const float* x, float center, float lambda, int mode,
                           const ganamd_critic_grads* grads, float* out, float* gx, float* norms, float* penalty,
-                          void* workspace, hipStream_t stream);
+                          void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Library identification (for load checks). */
 const char* ganamd_version(void);

@@ -12,11 +12,16 @@ critic's parameters after its step to the path given as argv[1].
 progan schedule (pipeline.Iteration, fake batches one per critic step on a side stream) at
 B = 64 per rank, one iteration; rank 0 writes both models' parameters and gradients.
 
-``dp_worker.py OUT graph``: the bench's N > 1 graph-mode path instead -- one pipelined WGAN-GP
-iteration (gan_amd.pipeline.Iteration: captured fake-batch / critic / AdamW / generator graphs,
-the next fake batch on a side stream, the flat-gradient all-reduce eagerly between graphs) at
-B = 8 per rank with device Philox streams seeded per rank; rank 0 writes both models' parameters
-and gradients after the iteration.
+``dp_worker.py OUT graph SCHEDULE [B]``: the bench's N > 1 graph-mode path instead -- one pipelined
+WGAN-GP iteration (gan_amd.pipeline.Iteration: captured fake-batch / critic / AdamW / generator
+graphs, the next fake batch on a side stream, the flat-gradient all-reduce eagerly between graphs)
+at B per rank (default 8; 64 = config 3's per-GPU batch) with device Philox streams seeded per rank;
+rank 0 writes both models' parameters and gradients after the iteration, and the first all-reduced
+critic gradient (before any AdamW step).
+
+Every mode records the FIRST all-reduced critic gradient of the timed iteration (``d_grad0``): the
+shard mean before any optimizer step, where a DP bug would show without the iteration's
+amplification of rounding differences.
 """
 import os
 import sys
@@ -80,6 +85,21 @@ def main(out):
 GRAPH_FAKE_GROUPS = (4, 1)
 
 
+class FirstAllreduce:
+    """The trainer's all-reduce (dist.allreduce_mean_) that keeps a copy of the first buffer it
+    reduces once ``armed`` -- the first critic gradient of the timed iteration."""
+
+    def __init__(self):
+        from gan_amd.dist import allreduce_mean_
+        self.fn, self.armed, self.first = allreduce_mean_, False, None
+
+    def __call__(self, flat):
+        self.fn(flat)
+        if self.armed and self.first is None:
+            self.first = flat.detach().cpu().clone()
+        return flat
+
+
 def main_graph(out):
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
@@ -92,19 +112,22 @@ def main_graph(out):
     # bench.py's N > 1 schedule: fake groups (4, 1), the second group made on the side stream while
     # the first group's critic steps and all-reduces run ("serial": the N = 1 order)
     serial = len(sys.argv) > 3 and sys.argv[3] == "serial"
-    it = Iteration(tr, B_GRAPH, 5, world, overlap=not serial, fake_groups=GRAPH_FAKE_GROUPS)
+    bs = int(sys.argv[4]) if len(sys.argv) > 4 else B_GRAPH
+    ar = FirstAllreduce()
+    it = Iteration(tr, bs, 5, world, overlap=not serial, fake_groups=GRAPH_FAKE_GROUPS, allreduce=ar)
     snap = snapshot(tr)
     it.eager()                     # warm-up (all-reduces included), then capture
     it.capture()
     restore(tr, snap)
     dist.barrier()
+    ar.armed = True
     it.step()
     torch.cuda.synchronize()
     res = {k: v.detach().cpu().clone() for k, v in
            (("g_data", tr.optimizer_G.flat.data), ("g_grad", tr.optimizer_G.flat.grad),
             ("d_data", tr.optimizer_D.flat.data), ("d_grad", tr.optimizer_D.flat.grad))}
     if rank == 0:
-        torch.save(dict(res, world=world), out)
+        torch.save(dict(res, world=world, d_grad0=ar.first, batch=bs), out)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -137,24 +160,26 @@ def main_progan(out):
     import gan_amd
     from gan_amd.pipeline import Iteration, restore, snapshot
     if os.environ.get("GANAMD_TEST_PATCH_MASK"):      # diagnosis: kernel selection A/B
-        gan_amd.ops.LIB.ganamd_conv_set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
+        gan_amd.ops.set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
     dev = torch.device("cuda", 0)
     G, D = make_progan(gan_amd, dev)
     tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, progan_seed(rank)))
     overlap = os.environ.get("GANAMD_TEST_PROGAN_OVERLAP", "1") != "0"     # diagnosis override
-    it = Iteration(tr, B_PROGAN, 5, world, overlap=overlap)    # bench.py's progan schedule (fake_schedule)
+    ar = FirstAllreduce()
+    it = Iteration(tr, B_PROGAN, 5, world, overlap=overlap, allreduce=ar)    # bench.py's progan schedule
     snap = snapshot(tr)
     it.eager()
     it.capture()
     restore(tr, snap)
     dist.barrier()
+    ar.armed = True
     it.step()
     torch.cuda.synchronize()
     res = {k: v.detach().cpu().clone() for k, v in
            (("g_data", tr.optimizer_G.flat.data), ("g_grad", tr.optimizer_G.flat.grad),
             ("d_data", tr.optimizer_D.flat.data), ("d_grad", tr.optimizer_D.flat.grad))}
     if rank == 0:
-        torch.save(dict(res, world=world), out)
+        torch.save(dict(res, world=world, d_grad0=ar.first), out)
     dist.barrier()
     dist.destroy_process_group()
 

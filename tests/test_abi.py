@@ -42,10 +42,10 @@ def test_library_is_gfx950():
 def test_invalid_arguments_rejected():
     from gan_amd import _lib
     L = _lib.LIB
-    d = _lib.ConvDesc(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)   # B = 0: invalid geometry
+    d = _lib.ConvDesc(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)   # B = 0: invalid geometry
     n = _lib.c_size_t(0)
     assert L.ganamd_conv_workspace(d, 0, n) == -1
-    assert L.ganamd_conv_fwd(d, None, None, None, None, None, 1.0, None, None, None) == -1
+    assert L.ganamd_conv_fwd(d, None, None, None, None, None, 1.0, None, None, 0, None) == -1
     assert L.ganamd_prelu_fwd(None, None, 0, 0, None, None) == -1
     assert L.ganamd_adamw(None, None, None, None, 0, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, None) == -1
 
@@ -53,12 +53,14 @@ def test_invalid_arguments_rejected():
 def test_workspace_sizes():
     from gan_amd import _lib
     L = _lib.LIB
-    d = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 0)
+    d = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 0, 0)
     n = _lib.c_size_t(0)
     assert L.ganamd_conv_workspace(d, _lib.CONV_DGRAD, n) == 0
     assert n.value >= 4 * 8 * 4 * (18 * 18 - 16 * 16)   # the frame-split dgrad's ring buffer (replication pad)
     assert L.ganamd_rowreduce_workspace(8, 4096) >= 8 * 3 * 4
-    bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 7)      # unknown math mode
+    bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 7, 0)   # unknown math mode
+    assert L.ganamd_conv_workspace(bad, _lib.CONV_FWD, n) == -1
+    bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 0, 8)   # unknown kernel_off bit
     assert L.ganamd_conv_workspace(bad, _lib.CONV_FWD, n) == -1
 
 
@@ -130,7 +132,7 @@ def _critic_op(kind, ins, **kw):
 def _critic_plan(ops, B=4, C0=3, H0=8, W0=8, S=1):
     from gan_amd import _lib
     t = (_lib.CriticOp * len(ops))(*ops)
-    return _lib.LIB.ganamd_critic_create(t, len(ops), B, C0, H0, W0, S, 0)
+    return _lib.LIB.ganamd_critic_create(t, len(ops), B, C0, H0, W0, S, 0, 0)
 
 
 def test_critic_engine_plan():
@@ -163,15 +165,18 @@ def test_critic_engine_plan():
         assert L.ganamd_critic_region_bytes(p, r, ctypes.byref(b)) == 0
         regions.append(b.value)
     assert sum(regions) == n.value and regions[1] == regions[2] == regions[3] >= 4 * sum(vals[:-1])
-    assert L.ganamd_critic_bind(p, 1, ctypes.c_void_p(fake)) == 0
+    assert L.ganamd_critic_bind(p, 1, ctypes.c_void_p(fake), regions[1] - 4) == -1      # region too small
+    assert L.ganamd_critic_bind(p, 1, ctypes.c_void_p(fake), regions[1]) == 0
     # a sweep whose regions are not all bound is refused before any launch
-    assert L.ganamd_critic_forward(p, ctypes.c_void_p(fake), None, None, None) == -1
+    assert L.ganamd_critic_forward(p, ctypes.c_void_p(fake), None, None, 0, None) == -1
+    # a contiguous workspace smaller than the query is refused before any launch
+    assert L.ganamd_critic_forward(p, ctypes.c_void_p(fake), None, ctypes.c_void_p(fake), n.value - 4, None) == -1
     ptr = ctypes.c_void_p()
     assert L.ganamd_critic_value(p, 0, 3, ctypes.byref(ptr)) == 0 and not ptr.value   # nothing run yet
     assert L.ganamd_critic_value(p, 4, 3, ctypes.byref(ptr)) == -1
     # sweeps out of order are refused before any launch
-    assert L.ganamd_critic_backward(p, None, None, None, ctypes.c_void_p(fake), None) == -1
-    assert L.ganamd_critic_tangent(p, ctypes.c_void_p(fake), None, ctypes.c_void_p(fake), None) == -1
+    assert L.ganamd_critic_backward(p, None, None, None, ctypes.c_void_p(fake), n.value, None) == -1
+    assert L.ganamd_critic_tangent(p, ctypes.c_void_p(fake), None, ctypes.c_void_p(fake), n.value, None) == -1
     L.ganamd_critic_destroy(p)
     bad = [
         good[:-1] + [_critic_op("conv", [9], cout=2, k=1, pad_mode=0, alpha=1.0, stride=1, w=fake)],  # output not [1][B]
@@ -183,3 +188,58 @@ def test_critic_engine_plan():
     for ops in bad:
         assert not _critic_plan(ops)
     assert not _critic_plan(good, B=6, S=4)          # segments must divide the batch
+
+
+def test_undersized_workspace_rejected():
+    """Every entry point that takes a workspace also takes its size and refuses (GANAMD_EINVAL, -1)
+    a workspace smaller than its own query -- before launching anything, so these calls with
+    never-dereferenced pointers are safe without a GPU.  (tests/test_ops_gpu.py::
+    test_workspace_bytes_enforced runs the same calls on real buffers: one byte short -> -1, the
+    queried size -> 0.)"""
+    from gan_amd import _lib, ops
+    L = _lib.LIB
+    f = ctypes.c_void_p(0x1000)               # never dereferenced: the size check comes first
+    st = None
+    # convs: a replicate-padded 3x3 (packs the weight into the workspace), a strided one (phased
+    # dgrad), a 1x1 linear (the BN-fused skinny GEMM)
+    for geo in (ops.conv_geo(4, 8, 16, 16, 8, 3, 1, 1), ops.conv_geo(4, 16, 32, 32, 16, 3, 2, 1),
+                ops.conv_geo(8, 64, 64, 64, 64, 3, 1, 1)):
+        d = geo.desc()
+        for op in (_lib.CONV_FWD, _lib.CONV_DGRAD, _lib.CONV_WGRAD):
+            need = geo.ws_bytes(op)
+            if need == 0:
+                continue
+            short = need - 1
+            if op == _lib.CONV_FWD:
+                assert L.ganamd_conv_fwd(d, f, f, None, None, None, 1.0, f, f, short, st) == -1
+                assert L.ganamd_conv_fwd(d, f, f, None, None, None, 1.0, f, None, 0, st) == -1
+                assert L.ganamd_conv_fwd_ex(d, f, f, None, None, None, 1.0, None, None, None, f, f, short, st) == -1
+            elif op == _lib.CONV_DGRAD:
+                assert L.ganamd_conv_dgrad(d, f, f, None, 1.0, f, f, short, st) == -1
+            else:
+                assert L.ganamd_conv_wgrad(d, f, f, None, None, 1.0, f, 0, f, short, st) == -1
+                assert L.ganamd_conv_wgrad2(d, f, f, f, f, 1.0, f, 0, f, short, st) == -1
+    lin = ops.linear_geo(16, 256, 256)
+    need = lin.ws_bytes(_lib.CONV_FWD)
+    assert need > 0
+    assert L.ganamd_linear_bn_act(lin.desc(), f, f, None, 1.0, f, f, None, f, f, 0.1, 1e-5, f, f, need - 1, st) == -1
+    # row reductions (BatchNorm, PReLU slope, bias gradients): ganamd_rowreduce_workspace
+    C, Ln = 8, 1 << 16
+    short = L.ganamd_rowreduce_workspace(C, Ln) - 1
+    assert L.ganamd_bn_act_fwd(f, C, Ln, f, f, None, None, None, 0.1, 1e-5, f, f, f, f, short, st) == -1
+    assert L.ganamd_bn_act_fwd_seg(f, C, Ln, 2, f, f, None, None, None, 0.1, 1e-5, f, f, f, f, f,
+                                   L.ganamd_rowreduce_workspace(2 * C, Ln // 2) - 1, st) == -1
+    assert L.ganamd_bn_act_bwd(f, f, C, Ln, f, f, None, f, f, f, f, f, None, 0, f, short, st) == -1
+    assert L.ganamd_prelu_bwd(f, f, f, C, Ln, f, f, 0, f, short, st) == -1
+    assert L.ganamd_prelu_bwd_bwd(f, None, f, f, f, C, Ln, f, None, f, f, short, st) == -1
+    assert L.ganamd_prelu_tangent(f, f, f, f, C, Ln, f, f, 0, f, short, st) == -1
+    assert L.ganamd_row_dot(f, None, C, Ln, f, 0, f, short, st) == -1
+    # penalty, MiniBatchStdDev, image batch
+    assert L.ganamd_gp_fwd(f, 8, 3 * 64 * 64, 1.0, 10.0, 0, f, f, f, L.ganamd_gp_workspace(8, 3 * 64 * 64) - 1, st) == -1
+    mb = L.ganamd_mbstd_workspace(2) - 1
+    assert L.ganamd_mbstd_fwd(f, 64, 4, 8, 16, 2, 4, f, 64, None, f, mb, st) == -1
+    assert L.ganamd_mbstd_bwd(f, 64, f, 64, 4, 8, 16, 2, 4, f, f, mb, st) == -1
+    assert L.ganamd_mbstd_tangent(f, f, 64, 4, 8, 16, 2, 4, f, 64, f, mb, st) == -1
+    assert L.ganamd_mbstd_adjoint(f, f, 64, f, f, 64, 4, 8, 16, 2, 4, f, f, mb, st) == -1
+    assert L.ganamd_image_batch(f, 2, 80, 80, None, f, f, 4, 64, f, f, 4, 64, f, f, f, f,
+                                L.ganamd_image_batch_workspace(2, 80, 64) - 1, st) == -1

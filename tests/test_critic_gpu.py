@@ -74,14 +74,14 @@ def test_mbstd_kernels(lib, C, B, H, S):
     y = torch.empty(C + 1, B, H, H, device=DEV)
     std = torch.empty(S, device=DEV)
     st = torch.cuda.current_stream().cuda_stream
-    assert L.ganamd_mbstd_fwd(ptr(xg), ld, C, B, H * H, S, 4, ptr(y), ld, ptr(std), ptr(ws), st) == 0
+    assert L.ganamd_mbstd_fwd(ptr(xg), ld, C, B, H * H, S, 4, ptr(y), ld, ptr(std), ptr(ws), ws.numel() * 4, st) == 0
     gx = torch.empty_like(xg)
-    assert L.ganamd_mbstd_bwd(ptr(xg), ld, ptr(gyg), ld, C, B, H * H, S, 4, ptr(gx), ptr(ws), st) == 0
+    assert L.ganamd_mbstd_bwd(ptr(xg), ld, ptr(gyg), ld, C, B, H * H, S, 4, ptr(gx), ptr(ws), ws.numel() * 4, st) == 0
     yd = torch.empty(C + 1, B, H, H, device=DEV)
-    assert L.ganamd_mbstd_tangent(ptr(xg), ptr(xdg), ld, C, B, H * H, S, 4, ptr(yd), ld, ptr(ws), st) == 0
+    assert L.ganamd_mbstd_tangent(ptr(xg), ptr(xdg), ld, C, B, H * H, S, 4, ptr(yd), ld, ptr(ws), ws.numel() * 4, st) == 0
     ax = torch.empty_like(xg)
     assert L.ganamd_mbstd_adjoint(ptr(xg), ptr(xdg), ld, ptr(gyg), ptr(ayg), ld, C, B, H * H, S, 4, ptr(ax), ptr(ws),
-                                  st) == 0
+                                  ws.numel() * 4, st) == 0
     torch.cuda.synchronize()
     assert rel(y, y_ref) < 1e-6
     assert rel(gx, gx_ref) < 1e-5
@@ -89,7 +89,7 @@ def test_mbstd_kernels(lib, C, B, H, S):
     assert rel(yd[C], yd_ref[C]) < 1e-4 and rel(yd, yd_ref) < 1e-5
     assert rel(ax, ax_ref) < 1e-4
     # invalid geometry is refused, not launched
-    assert L.ganamd_mbstd_fwd(ptr(xg), ld, C, B, H * H, S, 3, ptr(y), ld, None, ptr(ws), st) != 0
+    assert L.ganamd_mbstd_fwd(ptr(xg), ld, C, B, H * H, S, 3, ptr(y), ld, None, ptr(ws), ws.numel() * 4, st) != 0
 
 
 def test_act_and_fused_sweep_kernels(lib):
@@ -145,7 +145,7 @@ def test_prelu_tangent(lib):
     ga = torch.full((C,), 1.5, device=DEV)
     ws = torch.empty(L.ganamd_rowreduce_workspace(C, Ln) // 4 + 1, device=DEV)
     assert L.ganamd_prelu_tangent(ptr(d(xd)), ptr(d(gy)), ptr(d(x)), ptr(d(a)), C, Ln, ptr(yd), ptr(ga), 1, ptr(ws),
-                                  st) == 0
+                                  ws.numel() * 4, st) == 0
     torch.cuda.synchronize()
     assert rel(yd, yd_want) < 1e-7 and rel(ga, ga_want) < 1e-5
 
@@ -293,7 +293,7 @@ def test_engine_gp_step_single_call(gan):
     norms = torch.empty(B, device=DEV)
     rc = _lib.LIB.ganamd_critic_gp_step(run.plan, xd.data_ptr(), 1.0, 10.0, 0, grads, out.data_ptr(),
                                         gx.data_ptr(), norms.data_ptr(), pen.data_ptr(), ws.data_ptr(),
-                                        _lib.stream())
+                                        nbytes.value, _lib.stream())
     assert rc == 0
     torch.cuda.synchronize()
     got = _grads(D)
@@ -465,7 +465,8 @@ def test_engine_threads_and_capture(gan):
                 g.zero_()
             rc = _lib.LIB.ganamd_critic_gp_step(self.run.plan, self.x.data_ptr(), 1.0, 10.0, 0, self.grads,
                                                 self.out.data_ptr(), self.gx.data_ptr(), self.norms.data_ptr(),
-                                                self.pen.data_ptr(), self.ws.data_ptr(), _lib.stream())
+                                                self.pen.data_ptr(), self.ws.data_ptr(), self.ws.numel() * 4,
+                                                _lib.stream())
             assert rc == 0
 
         def snapshot(self):

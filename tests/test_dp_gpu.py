@@ -13,13 +13,19 @@ group on the side stream during the first group's critic steps and all-reduces -
 order -- all-reduce between captured graphs) on two ranks equals, after
 one full iteration (5 critic steps + generator step), the same iteration run here eagerly with the
 two shards one after another and their gradients averaged by hand before every optimizer step.
+At B = 8 per rank (both schedules) and at B = 64 per rank with the side stream on: config 3's
+per-GPU batch and its N > 1 default schedule (the 64-sample fifth fake forward beside critic steps
+1-4, their all-reduces and AdamW; two such ranks on one MI355X).  The first all-reduced critic
+gradient (before any AdamW step) must equal the shard mean at 1e-6.
 
 test_dp_progan_four_ranks_match_shard_mean: config 5's split (the progan pair on 4 ranks, 64 images
 each, BASELINE.json) through the bench's progan schedule (fake batch of the next critic step on a
-side stream) against the four shards run one after another with hand-averaged gradients -- within
-3x of how far that shard mean moves when its four shards are summed in the opposite order (gloo's
-ring sums four buffers in its own order, and the iteration amplifies last-bit differences; with
-GANAMD_TEST_PROGAN_WORLD=2 the bar is the 1e-5 of the two-rank tests, measured passing).
+side stream) against the four shards run one after another with hand-averaged gradients.  The
+FIRST all-reduced critic gradient -- before any AdamW step, where a DP bug shows unamplified --
+must equal the shard mean at 1e-6 (four fp32 buffers summed in gloo's ring order: one rounding
+per add).  After the whole iteration the bar is 3x of how far that shard mean moves when its four
+shards are summed in the opposite order (the iteration amplifies last-bit differences: AdamW's
+first update is ~lr * sign(g)); with GANAMD_TEST_PROGAN_WORLD=2 it is the 1e-5 of the two-rank tests.
 
 test_bench_two_ranks: ``bench.py --gpus 2 --backend gloo`` starts its own ranks and reports
 n_gpus 2 (it used to run one rank silently), in eager and in graph mode.
@@ -94,20 +100,22 @@ def test_dp_steps_match_shard_mean(tmp_path):
     assert _rel(got["g_grad"], g_want) < 1e-5
 
 
-@pytest.mark.parametrize("schedule", ["overlap", "serial"])
-def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
+@pytest.mark.parametrize("schedule,B", [("overlap", 8), ("serial", 8), ("overlap", 64)])
+def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule, B):
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()           # two B = 64 ranks share this GPU with this process's cache
     out = str(tmp_path / "rank0_graph.pt")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
-           "graph", schedule]
+           "graph", schedule, str(B)]
     r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = torch.load(out, weights_only=True)
-    assert got["world"] == 2
+    assert got["world"] == 2 and got["batch"] == B and got["d_grad0"] is not None
 
     import gan_amd
     dev = torch.device("cuda", 0)
-    B = dp_worker.B_GRAPH
     G, D = dp_worker.make_models(gan_amd, dev)
     tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev, 1))
     g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
@@ -122,6 +130,7 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
     def mean_into(flat_grad, gs):
         flat_grad.copy_(gs[0] + gs[1]).mul_(0.5)          # gloo: SUM, then * 1/N (dist.allreduce_mean_)
 
+    first = None
     for i in range(5):
         gs = []
         for r, rng in enumerate(rngs):
@@ -130,6 +139,8 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
             gs.append(tr.optimizer_D.flat.grad.detach().clone())
         assert _rel(gs[0].cpu(), gs[1].cpu()) > 1e-2       # the shards really differ
         mean_into(tr.optimizer_D.flat.grad, gs)
+        if first is None:
+            first = tr.optimizer_D.flat.grad.detach().cpu().clone()
         tr.optimizer_D.step()
     gs = []
     for rng in rngs:
@@ -142,10 +153,12 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
     want = {"g_data": tr.optimizer_G.flat.data, "g_grad": tr.optimizer_G.flat.grad,
             "d_data": tr.optimizer_D.flat.data, "d_grad": tr.optimizer_D.flat.grad}
     errs = {k: _rel(got[k], v.detach().cpu()) for k, v in want.items()}
+    errs["d_grad0"] = _rel(got["d_grad0"], first)
     # parameters relative to how far the iteration moved them
     errs["g_move"] = float((got["g_data"] - want["g_data"].cpu()).double().norm() / (want["g_data"].cpu() - g0).double().norm())
     errs["d_move"] = float((got["d_data"] - want["d_data"].cpu()).double().norm() / (want["d_data"].cpu() - d0).double().norm())
-    print("graph-mode DP vs shard mean:", errs)
+    print(f"graph-mode DP (B={B}/rank, {schedule}) vs shard mean:", errs)
+    assert errs["d_grad0"] < 1e-6, errs
     assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
     assert errs["g_move"] < 1e-4 and errs["d_move"] < 1e-4, errs
 
@@ -153,7 +166,8 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule):
 def _shard_mean_iteration(tr, rngs, B, groups, reverse=False):
     """One WGAN-GP iteration with the shards run one after another on the same weights and the
     gradients of every optimizer step averaged by hand (gloo: SUM, then * 1/N; ``reverse``: the
-    shards summed in the opposite order -- another legitimate fp32 rounding of the same mean)."""
+    shards summed in the opposite order -- another legitimate fp32 rounding of the same mean).
+    Returns the first averaged critic gradient (before any optimizer step), on the host."""
     n = len(rngs)
     for k in set(groups):
         tr.generate_fakes(k, B)    # warm-up: the workers' warm-up recorded the noise shapes
@@ -177,6 +191,8 @@ def _shard_mean_iteration(tr, rngs, B, groups, reverse=False):
             gs.append(tr.optimizer_D.flat.grad.detach().clone())
         assert _rel(gs[0].cpu(), gs[1].cpu()) > 1e-2       # the shards really differ
         mean_into(tr.optimizer_D.flat.grad, gs)
+        if i == 0:
+            first = tr.optimizer_D.flat.grad.detach().cpu().clone()
         tr.optimizer_D.step()
     gs = []
     for rng in rngs:
@@ -186,6 +202,7 @@ def _shard_mean_iteration(tr, rngs, B, groups, reverse=False):
     mean_into(tr.optimizer_G.flat.grad, gs)
     tr.optimizer_G.step()
     torch.cuda.synchronize()
+    return first
 
 
 def _dp_errors(got, tr, g0, d0):
@@ -210,7 +227,7 @@ def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
 
     import gan_amd
     if os.environ.get("GANAMD_TEST_PATCH_MASK"):      # diagnosis: kernel selection A/B (dp_worker too)
-        gan_amd.ops.LIB.ganamd_conv_set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
+        gan_amd.ops.set_patch(int(os.environ["GANAMD_TEST_PATCH_MASK"]))
     dev = torch.device("cuda", 0)
     B = dp_worker.B_PROGAN
 
@@ -219,12 +236,16 @@ def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
         tr = gan_amd.Train([], dev, 1, 256, G, "G3_progan", D, "D3_progan", rng=gan_amd.DeviceRNG(dev, 1))
         g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
         rngs = [gan_amd.DeviceRNG(dev, dp_worker.progan_seed(r)) for r in range(W)]
-        _shard_mean_iteration(tr, rngs, B, [1] * 5, reverse=reverse)
-        return tr, g0, d0
+        first = _shard_mean_iteration(tr, rngs, B, [1] * 5, reverse=reverse)
+        return tr, g0, d0, first
 
-    tr, g0, d0 = shard_mean(False)
+    tr, g0, d0, first = shard_mean(False)
     errs = _dp_errors(got, tr, g0, d0)
+    errs["d_grad0"] = _rel(got["d_grad0"], first)
     print(f"progan {W}-rank DP vs shard mean:", errs)
+    # the first all-reduced critic gradient: the shard mean before any AdamW step, up to the order
+    # in which the ranks' fp32 buffers are summed (a wrong shard, scale or bucket shows at O(1))
+    assert errs["d_grad0"] < 1e-6, errs
     if W <= 2:
         # two shards sum the same way in any order (fp32 addition commutes): bit-level agreement
         assert errs["g_grad"] < 1e-5 and errs["d_grad"] < 1e-5, errs
@@ -238,7 +259,7 @@ def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
                                                    ("g_grad", tr.optimizer_G.flat.grad),
                                                    ("d_data", tr.optimizer_D.flat.data),
                                                    ("d_grad", tr.optimizer_D.flat.grad))}
-    tr2, _, _ = shard_mean(True)
+    tr2, _, _, _ = shard_mean(True)
     spread = _dp_errors(mid, tr2, g0, d0)
     print(f"progan {W}-rank: shard mean vs the same with the shards summed in reverse:", spread)
     for k in ("g_grad", "d_grad", "g_data", "d_data", "g_move", "d_move"):

@@ -71,7 +71,32 @@ def test_g_step_b16(gan, P):
     t64 = fixture("f64_g16.npz")
     G, D = _pair(gan, P)
     tr = gan.Train([0] * 10, DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.ReplayRNG(421, DEV))
-    gen, g_loss = tr.generator_trainstep(16)
+    # The float64 forward of this step puts ONE PReLU input on the kink (make_f64.py KINK: the main
+    # mapping network's layer 10 = block0.mapping_network.net.32, sample 11, channel 209, z = 5.2e-7
+    # against |z| ~ 0.8): fp32's ~1e-6 forward rounding picks the branch, and the two branches'
+    # gradients differ by 2.8e-2 in that layer's BatchNorm bias and ~1.5e-2 in every mapping layer
+    # below it (a 1e-6 perturbation of the float64 forward there reproduces the GPU's numbers;
+    # tools/g16_map_diag.py).  The test reads the branch the GPU took from the sign of that
+    # layer's output element (PReLU keeps the sign: its slope there is positive) and holds the GPU
+    # to the float64 truth OF THAT BRANCH (g16_grads: z > 0; g16_grads_kink: the same step with that
+    # one PReLU derivative taken as the slope), at the same bars -- 2x the reference's / the fp32 spread.
+    mod = gan.generator_13_5
+    kink_act = G.block0.mapping_network.net[32]
+    seen = []
+    inner = mod._lin_bn_act
+
+    def spy(lin, bn, act, z):
+        out = inner(lin, bn, act, z)
+        if act is kink_act:
+            seen.append(float(out.detach()[209, 11]))           # [C][B] layout
+        return out
+    mod._lin_bn_act = spy
+    try:
+        gen, g_loss = tr.generator_trainstep(16)
+    finally:
+        mod._lin_bn_act = inner
+    assert len(seen) == 1, seen
+    assert float(kink_act.weight.detach()[209]) > 0
     names = [n for n, _, _ in P["g_params"]]
     rows = _rows(G, names)
     loss = float(g_loss.detach())
@@ -79,23 +104,13 @@ def test_g_step_b16(gan, P):
     assert rel_err(tensor_summary(gen), fx["gen"]) < 1e-3
     has = np.asarray([0 if np.isnan(r[0]) else 1 for r in rows])
     assert (has == fx["has_grad"]).all()
-    # The float64 forward of this step puts ONE PReLU input on the kink (make_f64.py KINK: the main
-    # mapping network's layer 10, sample 11, channel 209, z = 5.2e-7 against |z| ~ 0.8): fp32's
-    # ~1e-6 forward rounding picks the branch, and the two branches' gradients differ by 2.8e-2 in
-    # that layer's BatchNorm bias and ~1.5e-2 in every mapping layer below it (a 1e-6 perturbation
-    # of the float64 forward there reproduces the GPU's numbers exactly; tools/g16_map_diag.py).  The
-    # reference's fp32 run lands on the float64 branch, this build's on the other: the GPU is held
-    # to the float64 truth of the branch it took (g16_grads_kink: the same step with that one PReLU
-    # derivative taken as the slope), at the same bars -- 2x the reference's / the fp32 spread.
-    sides = {"float64 branch": t64["g16_grads"]}
-    if "g16_grads_kink" in t64.files:
-        sides["other branch at the kink"] = t64["g16_grads_kink"]
-    stats = {k: grad_norm_stats(rows, v) for k, v in sides.items()}
-    side = min(stats, key=lambda k: stats[k][3])
-    got = stats[side]
+    side = "float64 branch" if seen[0] > 0 else "other branch at the kink"
+    truth = t64["g16_grads"] if seen[0] > 0 else t64["g16_grads_kink"]
+    got = grad_norm_stats(rows, truth)
     worst = np.maximum(t64["ref_g16_stats"], t64["g16_fp32_spread"].max(axis=0))
     bars = [2 * w + 1e-5 for w in worst]
-    print("G-step B=16 vs f64 truth", stats, "->", side, "reference", t64["ref_g16_stats"], "bars", bars)
+    print(f"G-step B=16: kink element {seen[0]:.3e} -> {side}; vs its f64 truth {got}; "
+          f"reference {t64['ref_g16_stats']} bars {bars}")
     assert all(g <= b for g, b in zip(got, bars)), (side, got, bars)
     assert rel_err([loss], t64["g16_loss"]) <= 2 * max(float(t64["ref_g16_loss_err"]),
                                                        float(t64["g16_loss_fp32_spread"].max())) + 1e-6

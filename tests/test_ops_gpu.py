@@ -775,7 +775,7 @@ def test_conv_wgrad2_two_segments(ops, case):
     ws = _lib.workspace(geo.ws_bytes(_lib.CONV_WGRAD), DEV)
     xg, gyg = [cn(x) for x in xs], [cn(t) for t in gys]
     rc = _lib.LIB.ganamd_conv_wgrad2(geo.desc(), _lib.ptr(xg[0]), _lib.ptr(gyg[0]), _lib.ptr(xg[1]), _lib.ptr(gyg[1]),
-                                     alpha, _lib.ptr(out), 1, _lib.ptr(ws), _lib.stream())
+                                     alpha, _lib.ptr(out), 1, *_lib.ws(ws), _lib.stream())
     assert rc == 0
     assert rel(out, gw0 + ref) < 1e-5
 
@@ -965,3 +965,108 @@ def test_pool_sum_fanout(ops, C, B, n):
         la = (ta * cn(wt)).sum() + (b0 * cn(w0)).sum() + ((b1 * cn(w1)).sum() if use1 else 0)
         la.backward()
         assert rel(nc(a0.grad), g0) < 1e-5 and rel(nc(a1.grad), g1) < 1e-5
+
+
+# ---- the C ABI's workspace sizes and per-call kernel selection (VERDICT r04 weak #9a, #10) -----
+
+def test_workspace_bytes_enforced(ops):
+    """Every conv entry point refuses a workspace one byte short of its query (GANAMD_EINVAL, nothing
+    launched: the output keeps its sentinel) and runs with exactly the queried size."""
+    from gan_amd import _lib
+    L = _lib.LIB
+    st = _lib.stream()
+    for geo in (ops.conv_geo(4, 8, 16, 16, 8, 3, 1, 1), ops.conv_geo(4, 16, 32, 32, 16, 3, 2, 1)):
+        d = geo.desc()
+        x = torch.randn(geo.Cin, geo.B, geo.H, geo.W, device=DEV)
+        gy = torch.randn(geo.Cout, geo.B, geo.OH, geo.OW, device=DEV)
+        w = torch.randn(geo.Cout, geo.Cin, geo.K, geo.K, device=DEV)
+        calls = {
+            _lib.CONV_FWD: lambda out, ws, n: L.ganamd_conv_fwd(d, _lib.ptr(x), _lib.ptr(w), None, None, None, 1.0,
+                                                                _lib.ptr(out), ws, n, st),
+            _lib.CONV_DGRAD: lambda out, ws, n: L.ganamd_conv_dgrad(d, _lib.ptr(gy), _lib.ptr(w), None, 1.0,
+                                                                    _lib.ptr(out), ws, n, st),
+            _lib.CONV_WGRAD: lambda out, ws, n: L.ganamd_conv_wgrad(d, _lib.ptr(x), _lib.ptr(gy), None, None, 1.0,
+                                                                    _lib.ptr(out), 0, ws, n, st),
+        }
+        shapes = {_lib.CONV_FWD: gy.shape, _lib.CONV_DGRAD: x.shape, _lib.CONV_WGRAD: w.shape}
+        for op, call in calls.items():
+            need = geo.ws_bytes(op)
+            if need == 0:
+                continue
+            buf = torch.empty(need // 4 + 1, device=DEV)
+            out = torch.full(shapes[op], 7.0, device=DEV)
+            assert call(out, buf.data_ptr(), need - 1) == -1, (geo, op)
+            torch.cuda.synchronize()
+            assert bool((out == 7.0).all()), "a refused call launched"
+            assert call(out, buf.data_ptr(), need) == 0, (geo, op)
+            torch.cuda.synchronize()
+            assert not bool((out == 7.0).any())
+
+
+def test_kernel_selection_per_call_threads(ops):
+    """The kernel choice is part of each call's descriptor (kernel_off), not library state: two host
+    threads, each on its own HIP stream, one sending a patch-eligible conv to the split6 LDS-patch
+    kernel (kernel_off 0) and the other to the gather GEMM (kernel_off = all off), interleaved, each
+    get bit for bit what the same call gives single-threaded -- and the two kernels' results differ
+    in the last bits (the selection has teeth)."""
+    import threading
+    from gan_amd import _lib
+    L = _lib.LIB
+    geo = ops.conv_geo(32, 96, 64, 64, 96, 5, 1, 2)     # 256 patch blocks: one per CU
+    torch.manual_seed(5)
+    x = torch.randn(geo.Cin, geo.B, geo.H, geo.W, device=DEV)
+    w = torch.randn(geo.Cout, geo.Cin, geo.K, geo.K, device=DEV)
+    sx = torch.rand(geo.Cin, geo.B, device=DEV) + 0.5
+    sy = torch.rand(geo.Cout, geo.B, device=DEV) + 0.5
+    offs = (0, _lib.KERNEL_PATCH_FWD | _lib.KERNEL_PATCH_DGRAD | _lib.KERNEL_WGRAD_ROW)
+
+    def desc(off):
+        d = geo.desc()
+        return _lib.ConvDesc(*[getattr(d, n) for n, _ in _lib.ConvDesc._fields_[:-1]], off)
+
+    for off, kernel in zip(offs, (1, 0)):          # the plan each descriptor selects
+        info = (_lib.c_int * 11)()
+        assert L.ganamd_conv_plan_info(desc(off), _lib.CONV_FWD, 1, info) == 0 and info[10] == kernel
+
+    def run(off, out, s):
+        d = desc(off)
+        n = _lib.c_size_t(0)
+        assert L.ganamd_conv_workspace(d, _lib.CONV_FWD, n) == 0
+        buf = torch.empty(n.value // 4 + 1, device=DEV)
+        rc = L.ganamd_conv_fwd(d, _lib.ptr(x), _lib.ptr(w), None, _lib.ptr(sx), _lib.ptr(sy), 0.1, _lib.ptr(out),
+                               buf.data_ptr(), n.value, s.cuda_stream)
+        assert rc == 0
+        return buf
+
+    single = []
+    for off in offs:
+        y = torch.empty(geo.Cout, geo.B, geo.OH, geo.OW, device=DEV)
+        keep = run(off, y, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        single.append(y)
+        del keep
+    assert not torch.equal(single[0], single[1])
+    assert rel(single[0], single[1]) < 1e-6
+    outs = [[torch.empty_like(single[0]) for _ in range(6)] for _ in offs]
+    errs = []
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            keep = []
+            with torch.cuda.stream(s):
+                for y in outs[k]:
+                    keep.append(run(offs[k], y, s))
+            s.synchronize()
+        except Exception as e:          # noqa: BLE001 (reported below)
+            errs.append(e)
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for k in range(2):
+        for y in outs[k]:
+            assert torch.equal(y, single[k]), k

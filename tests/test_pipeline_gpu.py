@@ -6,7 +6,12 @@ test_pipelined_iteration_matches_eager  one replay of the captured iteration (fa
     next critic step on a side stream, double-buffered; critic graphs; AdamW graphs; generator
     step) and one eager iteration from the same state leave bit-identical parameters, gradients,
     AdamW moments, BatchNorm statistics and RNG offsets; the eager run's draws never share a
-    Philox counter.
+    Philox counter.  Case "bench" is bench.py's own timed schedule at its own batch: B = 64, fake
+    groups [4, 1] (one 256-sample segmented-BatchNorm generator forward + one 64-sample one), no
+    side stream at N = 1 -- the exact launch plans (B = 256 patch-conv grids, B = 64 split-K tails)
+    whose replay the headline number times.  The eager steps it is compared with are the trainer's
+    discriminator_backward / generator_backward, which test_critic_gpu.py::test_d_step_b64 and
+    test_headline_gpu.py::test_g_step_b64_vs_oracle hold to the B = 64 oracle.
 test_segmented_batchnorm_op / test_generate_fakes_matches_separate_batches  the batched fake
     generation (all n_critic fake batches from one generator forward with per-segment BatchNorm
     statistics) reproduces n separate generator calls.
@@ -40,12 +45,21 @@ def _state(tr):
     return [t.detach().clone() for t in training_state(tr)] + [o.clone() for o in tr.rng.state().values()]
 
 
-@pytest.mark.parametrize("mode", ["overlap", "phases", "batched"])
+# mode -> (batch, fake groups, side stream)
+MODES = {"overlap": (B, None, True), "phases": (B, None, False), "batched": (B, [1, 3, 1], True),
+         "bench": (64, [4, 1], False)}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 def test_pipelined_iteration_matches_eager(gan, mode):
     from gan_amd.pipeline import Iteration, restore, snapshot
+    bs, groups, overlap = MODES[mode]
+    if mode == "bench":          # bench.py's N = 1 default schedule, as bench.fake_schedule builds it
+        import bench
+        assert (tuple(groups), overlap) == (bench.FAKE_GROUPS, bench.FAKE_OVERLAP)
     G, D = dp_worker.make_models(gan, DEV)
     tr = gan.Train([], DEV, 1, 256, G, "G13_5", D, "D9_4", rng=gan.DeviceRNG(DEV, 2024))
-    it = Iteration(tr, B, n_critic=5, overlap=mode != "phases", fake_groups=[1, 3, 1] if mode == "batched" else None)
+    it = Iteration(tr, bs, n_critic=5, overlap=overlap, fake_groups=groups)
     it.eager()                      # warm-up: packed weights, noise shapes (bulk draws from here on)
     torch.cuda.synchronize()
     snap = snapshot(tr)
@@ -78,8 +92,10 @@ def test_pipelined_iteration_matches_eager(gan, mode):
     assert len(set(ctrs)) == len(ctrs), "two draws of one iteration share a Philox counter"
     kinds = {s for s, *_ in draws}
     assert kinds == {0, 1, 2}, kinds            # eps, generator z + noise, real batches
-    # per iteration: 5 eps, 6 z + 6 bulk noise draws (batched in groups 1, 3, 1: 4 + 4), 5 real batches
-    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 8 if mode == "batched" else 12, 5]
+    # per iteration: 5 eps, one z + one bulk noise draw per generator forward (one per fake group
+    # + the generator step: groups of 1 -> 6 + 6, groups 1, 3, 1 -> 4 + 4, groups 4, 1 -> 3 + 3), 5 real batches
+    n_fwd = len(groups or [1] * 5) + 1
+    assert [sum(1 for d in draws if d[0] == s) for s in (0, 1, 2)] == [5, 2 * n_fwd, 5]
 
 
 class _FixedNoise:

@@ -52,7 +52,7 @@ def gpu():
     G._run_bank = run_bank
     tr = gan_amd.Train([0] * 10, "cuda", 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.ReplayRNG(SEED, "cuda"))
     if os.environ.get("G16_PATCH") is not None:        # ganamd_conv_set_patch mask (0: gather GEMM only)
-        gan_amd.ops.LIB.ganamd_conv_set_patch(int(os.environ["G16_PATCH"]))
+        gan_amd.ops.set_patch(int(os.environ["G16_PATCH"]))
     gen, loss = tr.generator_backward(B)
     torch.cuda.synchronize()
     got["gw"] = got["gw"].T                       # [B, 256] like the oracle

@@ -1,0 +1,13 @@
+#!/bin/bash
+# r05b: patch-conv A/B (1 wave/SIMD instances) + the GPU tests touched by the ABI / parity changes
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+L=./-gan-_amd/libganamd.so
+V=tools/variants
+export GANAMD_HEARTBEAT=gpurun_out/r05b_heartbeat
+AB_SET=patch timeout -k 10 300 python3 -u tools/ab_shapes.py $L $V/p96w4nu.so $V/p96w4.so $V/p96w4mb16nu.so $V/p48w4.so $L > gpurun_out/r05b_ab.txt 2>&1 &&
+AB_SET=patch AB_ACC=1 timeout -k 10 200 python3 -u tools/ab_shapes.py $V/p96w4nu.so $V/p96w4mb16nu.so $V/p48w4.so > gpurun_out/r05b_acc.txt 2>&1 &&
+timeout -k 10 1500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_ops_gpu.py tests/test_critic_gpu.py tests/test_pipeline_gpu.py "tests/test_headline_gpu.py::test_g_step_b16" \
+  > gpurun_out/r05b_tests.log 2>&1
