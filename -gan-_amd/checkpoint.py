@@ -11,8 +11,9 @@ the loaded network).  Here ``generator`` / ``discriminator`` are ``state_dict()`
 reference's own parameter/buffer names (drop-in and reference modules load each other's), they
 are loaded IN PLACE (the flat-buffer views and the optimizers stay bound), and the optimizer
 moments and step counters are saved too, and so are the device RNG's stream offsets
-(``DeviceRNG.state()``: z / noise, eps and synthetic-data streams), so a resumed run continues the
-random sequence instead of redrawing the first run's numbers.  Everything is tensors/str/int, so
+(``DeviceRNG.state()``: z / noise, eps and synthetic-data streams) and its Philox key (``seed``;
+restored on load even when the resuming process was seeded differently), so a resumed run
+continues the random sequence instead of redrawing the first run's numbers.  Everything is tensors/str/int, so
 ``torch.load(..., weights_only=True)`` reads it.
 """
 from __future__ import annotations
@@ -55,6 +56,7 @@ class CheckpointMixin:
         rng = getattr(self, "rng", None)
         if hasattr(rng, "state"):
             state["rng"] = {str(k): v.detach().to("cpu") for k, v in rng.state().items()}
+            state["rng_seed"] = int(rng.seed)      # the offsets index THIS key's sequence
         path = ckpt_path(self.ckpt_root, self.generator_name, self.discriminator_name, train_name, e, ii)
         err = None
         if not _is_dist() or torch.distributed.get_rank() == 0:
@@ -98,6 +100,8 @@ class CheckpointMixin:
         self.epoch, self.i = int(ck["epoch"]), int(ck["i"])
         rng = getattr(self, "rng", None)
         if "rng" in ck and hasattr(rng, "set_state"):
+            if "rng_seed" in ck and hasattr(rng, "set_seed") and int(ck["rng_seed"]) != rng.seed:
+                rng.set_seed(int(ck["rng_seed"]))    # a process seeded otherwise resumes the saved key
             rng.set_state({int(k): v for k, v in ck["rng"].items()})
         return True
 

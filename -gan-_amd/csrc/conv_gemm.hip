@@ -1448,7 +1448,10 @@ int conv_bm(int M) {
   const double bar = 0.95 * c128;   // a smaller tile only for a clear win
   return (c96 < bar && c96 <= c64) ? 96 : (c64 < bar ? 64 : 128);
 }
-constexpr bool wide_tiles() { return false; }
+#ifndef GANAMD_WIDE
+#define GANAMD_WIDE 0   // 128x256 conv tiles for M > 96 (A/B builds)
+#endif
+constexpr bool wide_tiles() { return GANAMD_WIDE != 0; }
 int conv_bn(int bm, int) { return bm <= 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
 constexpr bool tile96() { return true; }
 constexpr bool big96() { return true; }

@@ -39,6 +39,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kOOB = (int)0x80000000;
 constexpr int KS = 32;                 // output pixels per K-step (one row segment: W % 32 == 0)
+#ifndef GANAMD_WROW_APAD
+#define GANAMD_WROW_APAD 0             // bf16 elements between the two substeps' A planes (A/B builds)
+#endif
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)std::min<long>(bytes, 0x7fffffff),
@@ -115,7 +118,10 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   // B row stride (bf16): 112 B (7 16-byte chunks) for 32-row blocks, 96 B (6 chunks) for 16-row
   // blocks -- the row strides whose window reads are conflict-free for each fragment's lane groups
   constexpr int LDB = MB == 32 ? 56 : 48;
-  constexpr int PSA = BM * 16, ABUF = 2 * 3 * PSA; // two 16-pixel substeps x three planes
+  // two 16-pixel substeps x three planes; the second substep's planes start GANAMD_WROW_APAD bf16
+  // further: at 3 * PSA = a multiple of 256 bytes the A stores of units g and g + 2 (same row, the two
+  // substeps) hit the same banks (ds_write_b128: 8 lanes = two rows x four units per LDS cycle)
+  constexpr int PSA = BM * 16, SSA = 3 * PSA + GANAMD_WROW_APAD, ABUF = 2 * SSA;
   constexpr int PSB = BJ * LDB, BBUF = 3 * PSB;
   constexpr int AU = BM * 4, AUT = (AU + NT - 1) / NT;   // A units: 8 pixels of one row
   constexpr int BU = BJ * 12, BUT = (BU + NT - 1) / NT;  // B units: 4 columns of one row (48 staged)
@@ -204,7 +210,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
           for (int q = 0; q < 8; ++q) v[q] *= S.sa[e];
         bf16x8 h, m, l;
         split3<8>(v, h, m, l);
-        unsigned short* d = &As[buf][(g >> 1) * 3 * PSA + aoff<MB>(r, g & 1)];
+        unsigned short* d = &As[buf][(g >> 1) * SSA + aoff<MB>(r, g & 1)];
         *reinterpret_cast<bf16x8*>(d) = h;
         *reinterpret_cast<bf16x8*>(d + PSA) = m;
         *reinterpret_cast<bf16x8*>(d + 2 * PSA) = l;
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   auto compute = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {                      // two 16-pixel substeps
-      const unsigned short* A = &As[buf][s * 3 * PSA + aoff<MB>(arow, fh)];
+      const unsigned short* A = &As[buf][s * SSA + aoff<MB>(arow, fh)];
       bf16x8 a[3];
       if constexpr (MB == 32) {
 #pragma unroll

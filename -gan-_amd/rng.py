@@ -86,6 +86,13 @@ class DeviceRNG:
         """Offsets of this generator and its forks (device tensors, cloned): restore with set_state."""
         return {s: r.offset.clone() for s, r in [(self.stream, self)] + [(f.stream, f) for f in self._forks.values()]}
 
+    def set_seed(self, seed: int):
+        """Re-key this generator and its forks (a resumed run continues the SAVED seed's sequence;
+        graphs captured before this keep the key they were captured with)."""
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        for f in self._forks.values():
+            f.set_seed(self.seed)
+
     def set_state(self, st):
         """Restore offsets saved by state() (forks missing here are created)."""
         self.offset.copy_(st[self.stream])

@@ -82,3 +82,19 @@ def test_checkpoint_restores_rng_streams(tmp_path):
     assert tr2.load_generator_ckpt(name)
     assert int(tr2.rng.offset) == 7
     assert int(tr2.rng.fork(2).offset) == (2 << rng.STREAM_SHIFT) + 11
+
+
+def test_checkpoint_restores_rng_seed(tmp_path):
+    """The offsets index the saved key's sequence: a trainer built with ANOTHER seed resumes the
+    saved seed (and its forks follow), so its next draws are the ones the first run would make."""
+    _pp, tr = _trainer(tmp_path)
+    tr.rng = gan_amd.DeviceRNG("cpu", seed=1234)
+    with torch.no_grad():
+        tr.rng.offset.fill_(5)
+    name = os.path.splitext(os.path.basename(tr.save_ckpt("WGANGP", 0, 0)))[0]
+    _pp2, tr2 = _trainer(tmp_path)
+    tr2.rng = gan_amd.DeviceRNG("cpu", seed=99)
+    data = tr2.rng.fork(2)
+    assert tr2.load_generator_ckpt(name)
+    assert tr2.rng.seed == 1234 and data.seed == 1234 and int(tr2.rng.offset) == 5
+

@@ -45,8 +45,7 @@ def main():
     t = e0.elapsed_time(e1) / 1e3 / a.reps
     sp = g.H * g.W if g.transposed else g.OH * g.OW
     flop = 2 * g.B * sp * g.Cin * g.Cout * g.K * g.K
-    print(f"{a.op} {g}: {t * 1e6:.1f} us  {flop / t / 1e12:.1f} TF/s  env={os.environ.get('GANAMD_WGRAD_BLOCKS')},"
-          f"{os.environ.get('GANAMD_CONV_BLOCKS')}")
+    print(f"{a.op} {g}: {t * 1e6:.1f} us  {flop / t / 1e12:.1f} TF/s  lib={os.path.basename(os.environ.get('GANAMD_SO', 'in-tree'))}")
 
 
 if __name__ == "__main__":

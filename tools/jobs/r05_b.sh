@@ -11,3 +11,4 @@ AB_SET=patch AB_ACC=1 timeout -k 10 200 python3 -u tools/ab_shapes.py $V/p96w4nu
 timeout -k 10 1500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_ops_gpu.py tests/test_critic_gpu.py tests/test_pipeline_gpu.py "tests/test_headline_gpu.py::test_g_step_b16" \
   > gpurun_out/r05b_tests.log 2>&1
+[ $? -eq 0 ] && AB_SET=dg timeout -k 10 300 python3 -u tools/ab_shapes.py $L $V/wide2.so $V/wide1.so $L > gpurun_out/r05b_ab_wide.txt 2>&1
