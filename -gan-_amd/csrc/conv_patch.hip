@@ -61,6 +61,15 @@ constexpr int kMaxScale = 1024;   // input channels whose scales the block stage
 #ifndef GANAMD_P_UNROLL4
 #define GANAMD_P_UNROLL4 1        // fully unroll the tap loop of 4-wave blocks
 #endif
+#ifndef GANAMD_P16_DEDUP
+#define GANAMD_P16_DEDUP 0        // 16x16 paths: two B fragment reads per 16 channels instead of three
+#endif
+#ifndef GANAMD_P64
+#define GANAMD_P64 0              // a 64-row tile for 48 < M <= 64 (else the 96-row one, a third empty)
+#endif
+#ifndef GANAMD_P64_NW
+#define GANAMD_P64_NW 8           // waves of a 64-row block at W = 64 (8: 2 along M x 4 along pixels)
+#endif
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
@@ -111,11 +120,12 @@ __device__ __forceinline__ int mfma_row(int lane, int r) {
 template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
 __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int NT = 64 * NW;
-  // waves along M: 12-wave 96-row blocks split the rows three ways (32 rows x 128 pixels per wave: a
-  // third of the weight fragments per wave, 3 waves per SIMD); otherwise every wave owns all rows
-  constexpr int WM = (BM == 96 && NW == 12) ? 3 : 1, WN = NW / WM;
-  constexpr int PW = NPIX / WN;                             // pixels per wave
   constexpr int MB = (BM % 32 == 0) ? (BM == 96 ? GANAMD_P96_MB : 32) : 16;   // MFMA block edge (48 rows: 16)
+  // waves along M: blocks of 4 waves per 32 rows (the 12-wave 96-row and 8-wave 64-row blocks) give
+  // each wave 32 rows x 128 pixels (a third / half of the weight fragments per wave, 3 / 2 waves per
+  // SIMD); otherwise every wave owns all rows
+  constexpr int WM = (MB == 32 && BM % 32 == 0 && NW == 4 * (BM / 32)) ? BM / 32 : 1, WN = NW / WM;
+  constexpr int PW = NPIX / WN;                             // pixels per wave
   constexpr int TM = BM / (MB * WM), TN = PW / MB, NR = MB == 32 ? 16 : 4;
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
   constexpr int TH = NPIX / TW, PAD = (KK - 1) / 2, T = KK * KK;
@@ -227,9 +237,19 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   // the three B fragments of column block j at tap offset toff
   auto b_frag = [&](const unsigned short* P, int toff, int j, bf16x8 (&f)[3]) {
     const int o = poff<MB>(posb[j] + toff, fhalf);
-    f[0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
-    f[1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
-    f[2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
+    if constexpr (MB == 16 && GANAMD_P16_DEDUP) {
+      // paired 16x16x32: a lane's three B fragments hold only two distinct planes -- h and
+      // X = (pair hi ? l : m) -- (h|h), (m|h), (m|l): read each once, the middle one is a select
+      const bf16x8 h = *reinterpret_cast<const bf16x8*>(&P[o]);
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
+      f[0] = h;
+      f[1] = fhi ? h : x;
+      f[2] = x;
+    } else {
+      f[0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
+      f[1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
+      f[2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
+    }
   };
 
   acc_t acc[TM][TN];
@@ -384,7 +404,7 @@ int occ_of() {
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
   if (a.W == 64) {
-    constexpr int NW = BM == 96 ? GANAMD_P96_NW : GANAMD_P48_NW;
+    constexpr int NW = BM == 96 ? GANAMD_P96_NW : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
     if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
       hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),
@@ -409,12 +429,15 @@ hipError_t dispatch(const Args& a, hipStream_t st, bool dry, int* occ) {
   const int bm = row_tile(a.M);
   if (bm == 48) return a.KK == 3 ? go_k<48, 3>(a, st, dry, occ) : go_k<48, 5>(a, st, dry, occ);
   if (bm == 96) return a.KK == 3 ? go_k<96, 3>(a, st, dry, occ) : go_k<96, 5>(a, st, dry, occ);
+#if GANAMD_P64
+  if (bm == 64) return a.KK == 3 ? go_k<64, 3>(a, st, dry, occ) : go_k<64, 5>(a, st, dry, occ);
+#endif
   return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-int row_tile(int M) { return M <= 0 ? 0 : M <= 48 ? 48 : M <= 96 ? 96 : 0; }
+int row_tile(int M) { return M <= 0 ? 0 : M <= 48 ? 48 : (GANAMD_P64 && M <= 64) ? 64 : M <= 96 ? 96 : 0; }
 
 int block_pixels(int W) { return W == 64 ? 512 : W == 32 ? 256 : 0; }
 

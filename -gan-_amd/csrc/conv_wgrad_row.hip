@@ -39,6 +39,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kOOB = (int)0x80000000;
 constexpr int KS = 32;                 // output pixels per K-step (one row segment: W % 32 == 0)
+#ifndef GANAMD_WROW_ALLK
+#define GANAMD_WROW_ALLK 0             // 3x3: one block runs all three kernel rows on one staged A (A/B builds)
+#endif
 #ifndef GANAMD_WROW_APAD
 #define GANAMD_WROW_APAD 0             // bf16 elements between the two substeps' A planes (A/B builds)
 #endif
@@ -111,7 +114,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int MB, int NW, int TN, int KK, bool SCALED>
+// ALLK: the block owns ALL K kernel rows: per K-step the output-gradient tile A is staged once and
+// the K input rows it meets (ih = oh + kh - pad) one after another through the double-buffered B
+// stage -- K times the products per staged A (accumulators K * K per column block).
+template <int MB, int NW, int TN, int KK, bool SCALED, bool ALLK = false>
 __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   constexpr int NT = 64 * NW, BM = NW * MB, BJ = TN * MB, PAD = (KK - 1) / 2, T = KK * KK;
   constexpr int SEG = KS + KK - 1;                 // staged input columns
@@ -132,7 +138,8 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j0 = blockIdx.x * BJ, m0 = blockIdx.y * BM;
-  const int kh = blockIdx.z / p.splits, split = blockIdx.z - kh * p.splits;
+  const int kh_blk = ALLK ? 0 : blockIdx.z / p.splits, split = ALLK ? blockIdx.z : blockIdx.z - kh_blk * p.splits;
+  constexpr int NKH = ALLK ? KK : 1;                 // kernel rows this block accumulates
   const int W = p.W, HW = p.H * W;
   const long L = (long)p.B * HW;                   // row length of a / x
   const int ks_seg = (int)(L / KS);
@@ -150,24 +157,39 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     f32x4 rb[BUT];
     float sa[AUT], sb[BUT];
   };
-  // global -> registers for K-step ks
-  auto gload = [&](int ks, Stage& S) {
+  struct KStep {                                   // where K-step ks reads
+    rsrc_t ra, rx;
+    long n0;
+    int b, oh, ow0;
+  };
+  auto kstep = [&](int ks) {
     const bool s2 = ks >= ks_seg;
     const int kl = s2 ? ks - ks_seg : ks;
-    const rsrc_t ra = s2 ? ra2 : ra1, rx = s2 ? rx2 : rx1;
-    const long n0 = (long)kl * KS;
-    const int b = (int)(n0 / HW), rem = (int)(n0 - (long)b * HW);
-    const int oh = rem / W, ow0 = rem - oh * W;
+    KStep k;
+    k.ra = s2 ? ra2 : ra1;
+    k.rx = s2 ? rx2 : rx1;
+    k.n0 = (long)kl * KS;
+    k.b = (int)(k.n0 / HW);
+    const int rem = (int)(k.n0 - (long)k.b * HW);
+    k.oh = rem / W;
+    k.ow0 = rem - k.oh * W;
+    return k;
+  };
+  // global -> registers: the A tile of K-step k ...
+  auto aload = [&](const KStep& k, Stage& S) {
 #pragma unroll
     for (int e = 0; e < AUT; ++e) {
       const int u = min(tid + e * NT, AU - 1), r = u >> 2, g = u & 3;
       const int m = m0 + r;
-      const int off = m < p.M ? (int)(4 * ((long)m * L + n0 + 8 * g)) : kOOB;
-      S.ra[e][0] = bload4(ra, off);
-      S.ra[e][1] = bload4(ra, off == kOOB ? kOOB : off + 16);
-      if (SCALED) S.sa[e] = bload(rsa, m < p.M ? 4 * (m * p.B + b) : kOOB);
+      const int off = m < p.M ? (int)(4 * ((long)m * L + k.n0 + 8 * g)) : kOOB;
+      S.ra[e][0] = bload4(k.ra, off);
+      S.ra[e][1] = bload4(k.ra, off == kOOB ? kOOB : off + 16);
+      if (SCALED) S.sa[e] = bload(rsa, m < p.M ? 4 * (m * p.B + k.b) : kOOB);
     }
-    int ih = oh + kh - PAD;
+  };
+  // ... and its input row segment for kernel row kh
+  auto bload_row = [&](const KStep& k, int kh, Stage& S) {
+    int ih = k.oh + kh - PAD;
     bool row_in = true;
     if (p.replicate)
       ih = min(max(ih, 0), p.H - 1);
@@ -177,23 +199,23 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     for (int e = 0; e < BUT; ++e) {
       const int u = min(tid + e * NT, BU - 1), jr = u / 12, cg = u - jr * 12;
       const int j = j0 + jr;
-      const long rowbase = (long)j * L + (long)b * HW + (long)ih * W;
+      const long rowbase = (long)j * L + (long)k.b * HW + (long)ih * W;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = 4 * cg + q;
-        int iw = ow0 - PAD + c;
+        int iw = k.ow0 - PAD + c;
         bool in = row_in && j < p.J && c < SEG;
         if (p.replicate)
           iw = min(max(iw, 0), W - 1);
         else
           in = in && iw >= 0 && iw < W;
-        S.rb[e][q] = bload(rx, in ? (int)(4 * (rowbase + iw)) : kOOB);
+        S.rb[e][q] = bload(k.rx, in ? (int)(4 * (rowbase + iw)) : kOOB);
       }
-      if (SCALED) S.sb[e] = bload(rsx, j < p.J ? 4 * (j * p.B + b) : kOOB);
+      if (SCALED) S.sb[e] = bload(rsx, j < p.J ? 4 * (j * p.B + k.b) : kOOB);
     }
   };
   // registers -> LDS (scaled, split into the three planes)
-  auto sstore = [&](int buf, const Stage& S) {
+  auto astore = [&](int buf, const Stage& S) {
 #pragma unroll
     for (int e = 0; e < AUT; ++e) {
       const int u = tid + e * NT;
@@ -216,6 +238,8 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
         *reinterpret_cast<bf16x8*>(d + 2 * PSA) = l;
       }
     }
+  };
+  auto bstore = [&](int buf, const Stage& S) {
 #pragma unroll
     for (int e = 0; e < BUT; ++e) {
       const int u = tid + e * NT;
@@ -235,13 +259,15 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     }
   };
 
-  acc_t acc[TN][KK];
+  acc_t acc[NKH][TN][KK];
 #pragma unroll
-  for (int jb = 0; jb < TN; ++jb)
+  for (int q = 0; q < NKH; ++q)
 #pragma unroll
-    for (int t = 0; t < KK; ++t)
+    for (int jb = 0; jb < TN; ++jb)
 #pragma unroll
-      for (int r = 0; r < NR; ++r) acc[jb][t][r] = 0.f;
+      for (int t = 0; t < KK; ++t)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[q][jb][t][r] = 0.f;
 
   // lane roles: 32x32 -- (r, h): A row r, k = 8h..8h+7; B column r.  16x16 paired -- (r, q):
   // half hf = q & 1 (k = 8hf..), pair hi = q >> 1: A (h|m), (h|l), (m|h); B (h|h), (m|h), (m|l)
@@ -249,10 +275,13 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   const int fh = MB == 32 ? (lane >> 5) : ((lane >> 4) & 1);
   const int hi = MB == 32 ? 0 : (lane >> 5);
   const int arow = wv * MB + fr;
-  auto compute = [&](int buf) {
+  // the products of the staged A (buffer abuf) with the staged input row (buffer bbuf) into the
+  // accumulators of kernel row QK
+  auto compute = [&](int abuf, int bbuf, auto QKc) {
+    constexpr int QK = decltype(QKc)::value;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {                      // two 16-pixel substeps
-      const unsigned short* A = &As[buf][s * SSA + aoff<MB>(arow, fh)];
+      const unsigned short* A = &As[abuf][s * SSA + aoff<MB>(arow, fh)];
       bf16x8 a[3];
       if constexpr (MB == 32) {
 #pragma unroll
@@ -264,7 +293,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
       }
 #pragma unroll
       for (int jb = 0; jb < TN; ++jb) {
-        const unsigned short* Bp = &Bs[buf][(jb * MB + fr) * LDB + 16 * s + 8 * fh];
+        const unsigned short* Bp = &Bs[bbuf][(jb * MB + fr) * LDB + 16 * s + 8 * fh];
         if constexpr (MB == 32) {
           u32x4 w[3][2];
 #pragma unroll
@@ -276,7 +305,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
             constexpr int kw = decltype(KWc)::value;
             const bf16x8 bh = shifted<kw>(w[0][0], w[0][1]), bm = shifted<kw>(w[1][0], w[1][1]),
                          bl = shifted<kw>(w[2][0], w[2][1]);
-            acc_t& c = acc[jb][kw];
+            acc_t& c = acc[QK][jb][kw];
             // l*h, h*l, m*m, m*h, h*m, h*h: smallest first into the same accumulator
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bh, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bl, c, 0, 0, 0);
@@ -293,7 +322,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
           static_for<0, KK>([&](auto KWc) {
             constexpr int kw = decltype(KWc)::value;
             const bf16x8 bh = shifted<kw>(wh0, wh1), bx = shifted<kw>(wx0, wx1);
-            acc_t& c = acc[jb][kw];
+            acc_t& c = acc[QK][jb][kw];
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bh, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], hi ? bh : bx, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bx, c, 0, 0, 0);
@@ -304,40 +333,90 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   };
 
   if (k0 < k1) {
-    Stage s0;
-    gload(k0, s0);
-    sstore(0, s0);
-    __syncthreads();
-    for (int ks = k0; ks < k1; ++ks) {
-      const int buf = (ks - k0) & 1;
-      const bool more = ks + 1 < k1;
-      if (more) gload(ks + 1, s0);
-      compute(buf);
-      if (more) sstore(buf ^ 1, s0);
+    if constexpr (!ALLK) {
+      Stage s0;
+      {
+        const KStep k = kstep(k0);
+        aload(k, s0);
+        bload_row(k, kh_blk, s0);
+      }
+      astore(0, s0);
+      bstore(0, s0);
       __syncthreads();
+      for (int ks = k0; ks < k1; ++ks) {
+        const int buf = (ks - k0) & 1;
+        const bool more = ks + 1 < k1;
+        if (more) {
+          const KStep k = kstep(ks + 1);
+          aload(k, s0);
+          bload_row(k, kh_blk, s0);
+        }
+        compute(buf, buf, std::integral_constant<int, 0>{});
+        if (more) {
+          astore(buf ^ 1, s0);
+          bstore(buf ^ 1, s0);
+        }
+        __syncthreads();
+      }
+    } else {
+      // units u = (ks, kh) in order; A double-buffered per K-step, B per unit
+      Stage s0;
+      KStep k = kstep(k0);
+      aload(k, s0);
+      bload_row(k, 0, s0);
+      astore(0, s0);
+      bstore(0, s0);
+      __syncthreads();
+      int bb = 0;
+      for (int ks = k0; ks < k1; ++ks) {
+        const int ab = (ks - k0) & 1;
+        const bool more = ks + 1 < k1;
+        static_for<0, KK>([&](auto QKc) {
+          constexpr int kh = decltype(QKc)::value;
+          const bool next = kh + 1 < KK || more;        // a unit after this one
+          if (kh + 1 < KK) {
+            bload_row(k, kh + 1, s0);
+          } else if (more) {
+            k = kstep(ks + 1);
+            aload(k, s0);
+            bload_row(k, 0, s0);
+          }
+          compute(ab, bb, QKc);
+          if (next) {
+            bstore(bb ^ 1, s0);
+            if (kh + 1 == KK) astore(ab ^ 1, s0);
+          }
+          __syncthreads();
+          bb ^= 1;
+        });
+      }
     }
   }
 
   // epilogue: every block writes its whole tile (zeros for an empty K range)
   const long numel = (long)p.M * p.J * T;
 #pragma unroll
-  for (int jb = 0; jb < TN; ++jb) {
-    const int j = j0 + jb * MB + (lane & (MB - 1));
-    if (j >= p.J) continue;
+  for (int q = 0; q < NKH; ++q) {
+    const int kh = ALLK ? q : kh_blk;
 #pragma unroll
-    for (int kw = 0; kw < KK; ++kw) {
+    for (int jb = 0; jb < TN; ++jb) {
+      const int j = j0 + jb * MB + (lane & (MB - 1));
+      if (j >= p.J) continue;
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int m = m0 + wv * MB + mfma_row<MB>(lane, r);
-        if (m >= p.M) continue;
-        const long o = ((long)m * p.J + j) * T + kh * KK + kw;
-        const float v = p.alpha * acc[jb][kw][r];
-        if (p.slab)
-          p.slab[(long)split * numel + o] = v;
-        else if (p.accumulate)
-          p.out[o] += v;
-        else
-          p.out[o] = v;
+      for (int kw = 0; kw < KK; ++kw) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int m = m0 + wv * MB + mfma_row<MB>(lane, r);
+          if (m >= p.M) continue;
+          const long o = ((long)m * p.J + j) * T + kh * KK + kw;
+          const float v = p.alpha * acc[q][jb][kw][r];
+          if (p.slab)
+            p.slab[(long)split * numel + o] = v;
+          else if (p.accumulate)
+            p.out[o] += v;
+          else
+            p.out[o] = v;
+        }
       }
     }
   }
@@ -352,10 +431,14 @@ Tile tile_of(int M) {
   return {32, (M + 31) / 32, 1};
 }
 
+// whether a launch of K x K taps runs all kernel rows per block (a function of the geometry alone)
+constexpr bool all_rows(int KK) { return GANAMD_WROW_ALLK && KK == 3; }
+
 template <int MB, int NW, int TN, int KK, bool S>
 hipError_t go(const Args& a, hipStream_t st) {
-  const dim3 grid((a.J + TN * MB - 1) / (TN * MB), (a.M + NW * MB - 1) / (NW * MB), KK * a.splits);
-  hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S>), grid, dim3(64 * NW), 0, st, a);
+  constexpr bool AK = all_rows(KK);
+  const dim3 grid((a.J + TN * MB - 1) / (TN * MB), (a.M + NW * MB - 1) / (NW * MB), (AK ? 1 : KK) * a.splits);
+  hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK>), grid, dim3(64 * NW), 0, st, a);
   return hipGetLastError();
 }
 
@@ -382,7 +465,8 @@ bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW, int
 // CU), each split at least 16 K-steps (512 pixels).
 void plan(int M, int J, int B, int H, int W, int K, int segs, int cus, int* splits, int* ks_per_split) {
   const Tile t = tile_of(M);
-  const long tiles = (long)((J + t.tn * t.mb - 1) / (t.tn * t.mb)) * ((M + t.nw * t.mb - 1) / (t.nw * t.mb)) * K;
+  const long tiles = (long)((J + t.tn * t.mb - 1) / (t.tn * t.mb)) * ((M + t.nw * t.mb - 1) / (t.nw * t.mb)) *
+                     (all_rows(K) ? 1 : K);
   const long ks_total = (long)segs * B * H * W / KS;
   const long target = 4L * cus;
   long s = std::max<long>(1, (target + tiles - 1) / tiles);

@@ -178,6 +178,9 @@ def cpu_baseline(threads, B=8):
     t_iter = N_CRITIC * sum(t_d) / len(t_d) + t_g
     return {"value": B / t_iter, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "note": "not 2 full iterations (BASELINE.md §4): 2 x (5 D-steps + 1 G-step) at B=8 is ~90 s of CPU per "
+                    "bench run, past the bounded sample the bench contract allows (10-30 s); the per-step times "
+                    "are timed and combined as 5 * mean(t_D) + t_G",
             "sample": f"CPU oracle (fp32 PyTorch-CPU restatement of the reference step), B={B}: 1 warm-up D-step + "
                       f"G-step, then D-steps {', '.join(f'{t:.2f}s' for t in t_d)} and G-step {t_g:.2f}s timed; "
                       f"t_iter = 5*mean(t_D) + t_G = {t_iter:.1f}s"}
@@ -188,10 +191,14 @@ def cpu_baseline(threads, B=8):
 # rocprofv3 kernel trace reports; back-to-back launches also give the sustained rate):
 #   probe     D9_4's mid-level block conv, 128->128 channels, 3x3 replication pad, 32x32, at
 #             B = 96: 768 output tiles = one round of the kernel's resident blocks, so it is ONE
-#             conv_gemm_kernel<128,128,2,2,1,false,false> launch (whole tiles, no split-K);
-#   dominant  the kernel with the largest share of the iteration's GPU time in the rocprof trace:
-#             G13_5's 96-channel 5x5 modulated conv at 64x64 (x*s on the gather, *d in the
-#             epilogue), B = 64: conv_gemm_kernel<96,128,1,4,1,true,false>.
+#             launch of the critic's gather GEMM conv_gemm_kernel<128,128,2,2,1,false,false> --
+#             the top kernel INSTANCE of the iteration trace (profiles/r04_iteration_summary.txt:
+#             0.124 s over 1,020 launches of many shapes);
+#   dominant  G13_5's 96-channel 5x5 modulated conv at 64x64 (x*s on the patch, *d in the
+#             epilogue), B = 64: one launch of the split6 LDS-patch conv conv_patch_x3_kernel<96,...>
+#             -- the top kernel FAMILY (the patch conv: 0.58 s of the iteration's 1.89 s busy) and
+#             the top single shape (0.110 s over 30 launches).  The line carries both; `top_instance`
+#             says which of them leads the committed trace by instance.
 PROBES = {
     "probe": dict(B=96, cin=128, h=32, cout=128, k=3, scaled=False,
                   shape="conv fwd B=96 128->128 3x3 replicate-pad 32x32 (D9_4 block conv; 768 whole tiles, one launch)"),
@@ -263,6 +270,13 @@ def probe_kernel(dev, spec, reps=20):
                       f"{reps} launches between two events"}
 
 
+# Which probed kernel leads the committed iteration trace by instance (kernel name with template
+# arguments; tools/trace_summary.py), and by family -- from the profile of this round's build.
+TOP_INSTANCE = {"kernel": "conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", "probe": "critic_probe",
+                "iteration_s": 0.124, "launches": 1020, "family_top": "ganamd_patch::conv_patch_x3_kernel",
+                "family_s": 0.581, "source": "profiles/r04_iteration_summary.txt"}
+
+
 def roofline_probe(dev):
     """The line's roofline object is the DOMINANT kernel's; the critic probe rides along."""
     out = probe_kernel(dev, PROBES["dominant"])
@@ -275,6 +289,7 @@ def roofline_probe(dev):
             out["algorithmic_bytes_per_launch"] = t.get("algorithmic_bytes")
             out["traffic_source"] = t.get("source")
     out["critic_probe"] = probe_kernel(dev, PROBES["probe"])
+    out["top_instance"] = TOP_INSTANCE
     return out
 
 

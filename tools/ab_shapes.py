@@ -23,6 +23,10 @@ SHAPES_WGRAD = [
     ("wgrad", 128, 1025, 4, 1025, 3, 1, 1, False, 30),
     ("fwd", 64, 108, 64, 3, 5, 1, 2, False, 12),
     ("dgrad", 64, 48, 64, 48, 5, 1, 2, True, 20),
+    ("wgrad", 128, 64, 64, 64, 3, 1, 1, False, 25),
+    ("wgrad", 64, 64, 64, 64, 3, 1, 1, False, 50),
+    ("wgrad", 128, 128, 32, 128, 3, 1, 1, False, 25),
+    ("wgrad", 64, 128, 32, 128, 3, 1, 1, False, 50),
 ]
 SHAPES_DG = [   # fwd vs dgrad vs wgrad of the same critic convs (AB_SET=dg)
     ("fwd", 128, 64, 64, 64, 3, 1, 1, False, 25),

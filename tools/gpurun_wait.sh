@@ -6,7 +6,7 @@ T=$1; CMD=$2; LOG=$3
 for i in $(seq 1 12); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if [ $rc -ne 3 ] && ! grep -q "no free box right now" "$LOG"; then exit $rc; fi
+  if [ $rc -ne 3 ] && ! grep -q "status=transient" "$LOG"; then exit $rc; fi
   echo "[gpurun_wait] no box (try $i), retrying in 180 s" >> "$LOG.wait"
   sleep 180
 done
