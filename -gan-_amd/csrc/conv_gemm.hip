@@ -1043,7 +1043,9 @@ __device__ __forceinline__ void conv_body_x3(const ConvArgs& p) {
 template <int BM, int BN, int WGM, int WGN, int MODE, bool BSCALE, bool BF16>
 // (the bf16 body with per-(channel, sample) scales needs more than 3 waves/SIMD's registers: it spilled
 // 12-101 VGPRs there; 2 waves/SIMD -- except the 128x256 tile, which spills at 2 and not at 3)
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(BF16 && BSCALE && BM * BN < 128 * 256 ? 2 : GANAMD_CONV_WPE)))
+// (the fp32 128x256 tile runs at 2 waves/SIMD: 250 VGPRs, no spill)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(
+    (BF16 && BSCALE && BM * BN < 128 * 256) || (!BF16 && BM == 128 && BN == 256) ? 2 : GANAMD_CONV_WPE)))
 void conv_gemm_kernel(ConvArgs p) {
   if constexpr (BF16) {
     conv_body_bf16<BM, BN, WGM, WGN, MODE, BSCALE>(p);
@@ -1449,10 +1451,16 @@ int conv_bm(int M) {
   return (c96 < bar && c96 <= c64) ? 96 : (c64 < bar ? 64 : 128);
 }
 #ifndef GANAMD_WIDE
-#define GANAMD_WIDE 0   // 128x256 conv tiles for M > 96 (A/B builds)
+#define GANAMD_WIDE 1   // 128x256 tiles (2 waves/SIMD) for the unscaled fp32 GEMMs with 128-row tiles
 #endif
 constexpr bool wide_tiles() { return GANAMD_WIDE != 0; }
-int conv_bn(int bm, int) { return bm <= 32 ? 256 : (bm == 128 && wide_tiles()) ? 256 : 128; }
+// The 128x256 split6 tile at 2 waves/SIMD: the critic's 128- to 1025-channel convs (measured vs the
+// 128x128 tile at 3 waves/SIMD: 128->128 3x3 at 32x32 fwd 160 -> 183 TF/s, dgrad 107 -> 118;
+// 256->256 at 16x16 fwd 148 -> 159, dgrad 92 -> 100; profiles/r05_ab_wide.txt).  Not for scaled
+// (modulated) GEMMs -- their per-(channel, sample) scale loads spill it -- nor bf16 math.
+int conv_bn(int bm, bool bscale, bool bf16) {
+  return bm <= 32 ? 256 : (bm == 128 && wide_tiles() && !bscale && !bf16) ? 256 : 128;
+}
 constexpr bool tile96() { return true; }
 constexpr bool big96() { return true; }
 int wgrad_bm(int M, bool scaled) { return M <= 32 ? 32 : M <= 64 ? 64 : (M <= 96 || scaled) ? (M <= 96 ? 96 : 64) : 128; }
@@ -1498,9 +1506,11 @@ Plan split_plan(int bm, int bn, int tiles, int kt_total, double kflop, long out_
   return Plan{bm, bn, (kt_total + per - 1) / per, per};
 }
 
+// (bn: the unscaled fp32 tile; conv_plan picks the launch's own with conv_bn -- the packed operand
+// depends on bm alone)
 void conv_tile(int M, int* bm, int* bn) {
   *bm = conv_bm(M);
-  *bn = conv_bn(*bm, 0);
+  *bn = conv_bn(*bm, false, false);
 }
 
 // Resident blocks per CU of a kernel instance (the runtime's occupancy calculator; without a
@@ -1540,7 +1550,10 @@ int conv_occ_tile(int bm, int bn) {
       return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
     case 64: return conv_occ<64, 128, 2, 2, MODE, BSCALE, BF16>();
     case 96: return conv_occ<96, 128, 1, 4, MODE, BSCALE, BF16>();
-    default: return bn == 256 ? conv_occ<128, 256, 2, 2, MODE, BSCALE, BF16>() : conv_occ<128, 128, 2, 2, MODE, BSCALE, BF16>();
+    default:
+      if constexpr (!BSCALE && !BF16)
+        if (bn == 256) return conv_occ<128, 256, 2, 2, MODE, BSCALE, BF16>();
+      return conv_occ<128, 128, 2, 2, MODE, BSCALE, BF16>();
   }
 }
 
@@ -1599,11 +1612,12 @@ constexpr double kSustainedTflopsBf16 = 300.0;   // the bf16-LDS body (conv_body
 ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {
   ConvPlan pl{};
   conv_tile(M, &pl.bm, &pl.bn);
+  pl.bn = conv_bn(pl.bm, bscale, bf16);
   // the bf16 body has 32x32 blocks only: its 48-row GEMMs run on the 64-row tile over the same
   // 48-row packed operand (rows past it read as 0 through the buffer bound, are not stored)
   if (bf16 && pl.bm == 48) {
     pl.bm = 64;
-    pl.bn = conv_bn(64, 0);
+    pl.bn = conv_bn(64, bscale, bf16);
   }
   if (bf16 && pl.bm == 16) pl.bm = 32;
   pl.gx = (N + pl.bn - 1) / pl.bn;
@@ -1851,8 +1865,9 @@ hipError_t dispatch_conv_tile(const ConvArgs& p, const ConvPlan& pl, float* slab
     case 64: return launch_conv<64, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
     case 96: return launch_conv<96, 128, 1, 4, MODE, BSCALE, BF16>(p, pl, slab, st);
     default:
-      return pl.bn == 256 ? launch_conv<128, 256, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st)
-                          : launch_conv<128, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
+      if constexpr (!BSCALE && !BF16)   // (conv_bn: the wide tile is for unscaled fp32 GEMMs only)
+        if (pl.bn == 256) return launch_conv<128, 256, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
+      return launch_conv<128, 128, 2, 2, MODE, BSCALE, BF16>(p, pl, slab, st);
   }
 }
 

@@ -59,13 +59,16 @@ constexpr int kMaxScale = 1024;   // input channels whose scales the block stage
 #define GANAMD_P48_NW 8           // waves of a 48-row block at W = 64
 #endif
 #ifndef GANAMD_P_UNROLL4
-#define GANAMD_P_UNROLL4 1        // fully unroll the tap loop of 4-wave blocks
+#define GANAMD_P_UNROLL4 1        // fully unroll the tap loop of the 4-wave 5x5 blocks (3x3: a loop of tap pairs)
 #endif
 #ifndef GANAMD_P16_DEDUP
 #define GANAMD_P16_DEDUP 0        // 16x16 paths: two B fragment reads per 16 channels instead of three
 #endif
 #ifndef GANAMD_P64
-#define GANAMD_P64 0              // a 64-row tile for 48 < M <= 64 (else the 96-row one, a third empty)
+#define GANAMD_P64 1              // a 64-row tile for 48 < M <= 64 (else the 96-row one, a third empty)
+#endif
+#ifndef GANAMD_P128
+#define GANAMD_P128 0             // a 128-row tile for 96 < M <= 128 (else the gather GEMM takes the conv)
 #endif
 #ifndef GANAMD_P64_NW
 #define GANAMD_P64_NW 8           // waves of a 64-row block at W = 64 (8: 2 along M x 4 along pixels)
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   // waves along M: blocks of 4 waves per 32 rows (the 12-wave 96-row and 8-wave 64-row blocks) give
   // each wave 32 rows x 128 pixels (a third / half of the weight fragments per wave, 3 / 2 waves per
   // SIMD); otherwise every wave owns all rows
-  constexpr int WM = (MB == 32 && BM % 32 == 0 && NW == 4 * (BM / 32)) ? BM / 32 : 1, WN = NW / WM;
+  constexpr int WM = (MB == 32 && NW % 4 == 0 && BM % (32 * (NW / 4)) == 0) ? NW / 4 : 1, WN = NW / WM;
   constexpr int PW = NPIX / WN;                             // pixels per wave
   constexpr int TM = BM / (MB * WM), TN = PW / MB, NR = MB == 32 ? 16 : 4;
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
@@ -352,10 +355,12 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
       }
     };
     // the tap loop: fully unrolled where the registers allow it (48-row blocks, the 4-wave W = 32
-    // blocks: the taps' index math, weight prefetch and patch stores resolve at compile time and the
-    // next tap's fragment reads can be scheduled under the current tap's products); the 12-wave 96-row
-    // blocks spill when unrolled (or with the first taps peeled) and keep a loop of two taps
-    if constexpr (BM == 48 || (NW == 4 && GANAMD_P_UNROLL4)) {
+    // 5x5 blocks: the taps' index math, weight prefetch and patch stores resolve at compile time and
+    // the next tap's fragment reads can be scheduled under the current tap's products); the 12-wave
+    // 96-row blocks spill when unrolled (or with the first taps peeled) and keep a loop of two taps,
+    // and so do the 4-wave 3x3 blocks (measured: 96->96 3x3 at 32x32, B = 256, 117 -> 151 TF/s as a
+    // loop; profiles/r05_ab_patch.txt)
+    if constexpr (BM == 48 || (NW == 4 && KK == 5 && GANAMD_P_UNROLL4)) {
 #pragma unroll
       for (int t = 0; t < T; t += 2) tap_pair(t);
     } else {
@@ -404,16 +409,17 @@ int occ_of() {
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
   if (a.W == 64) {
-    constexpr int NW = BM == 96 ? GANAMD_P96_NW : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
+    constexpr int NW = BM == 128 ? 8 : BM == 96 ? GANAMD_P96_NW : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
     if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
       hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),
                          dim3(64 * NW), 0, st, a);
   } else {
-    if (occ) *occ = occ_of<BM, 4, 256, KK, 32, BSCALE, DGRAD>();
+    constexpr int NW = BM == 128 ? 8 : 4;     // 128 rows: 2 waves along M x 4 along pixels
+    if (occ) *occ = occ_of<BM, NW, 256, KK, 32, BSCALE, DGRAD>();
     if (!dry)
-      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, 4, 256, KK, 32, BSCALE, DGRAD>), dim3((unsigned)blocks(a)), dim3(256),
-                         0, st, a);
+      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 256, KK, 32, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),
+                         dim3(64 * NW), 0, st, a);
   }
   return dry ? hipSuccess : hipGetLastError();
 }
@@ -432,12 +438,17 @@ hipError_t dispatch(const Args& a, hipStream_t st, bool dry, int* occ) {
 #if GANAMD_P64
   if (bm == 64) return a.KK == 3 ? go_k<64, 3>(a, st, dry, occ) : go_k<64, 5>(a, st, dry, occ);
 #endif
+#if GANAMD_P128
+  if (bm == 128) return a.KK == 3 ? go_k<128, 3>(a, st, dry, occ) : go_k<128, 5>(a, st, dry, occ);
+#endif
   return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-int row_tile(int M) { return M <= 0 ? 0 : M <= 48 ? 48 : (GANAMD_P64 && M <= 64) ? 64 : M <= 96 ? 96 : 0; }
+int row_tile(int M) {
+  return M <= 0 ? 0 : M <= 48 ? 48 : (GANAMD_P64 && M <= 64) ? 64 : M <= 96 ? 96 : (GANAMD_P128 && M <= 128) ? 128 : 0;
+}
 
 int block_pixels(int W) { return W == 64 ? 512 : W == 32 ? 256 : 0; }
 

@@ -40,7 +40,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kOOB = (int)0x80000000;
 constexpr int KS = 32;                 // output pixels per K-step (one row segment: W % 32 == 0)
 #ifndef GANAMD_WROW_ALLK
-#define GANAMD_WROW_ALLK 0             // 3x3: one block runs all three kernel rows on one staged A (A/B builds)
+#define GANAMD_WROW_ALLK 1             // 3x3: one block runs all three kernel rows on one staged A (all_rows)
 #endif
 #ifndef GANAMD_WROW_APAD
 #define GANAMD_WROW_APAD 0             // bf16 elements between the two substeps' A planes (A/B builds)
@@ -431,12 +431,16 @@ Tile tile_of(int M) {
   return {32, (M + 31) / 32, 1};
 }
 
-// whether a launch of K x K taps runs all kernel rows per block (a function of the geometry alone)
-constexpr bool all_rows(int KK) { return GANAMD_WROW_ALLK && KK == 3; }
+// Whether a launch runs all kernel rows per block (a function of the geometry alone): the 3x3 weight
+// gradients of 64 output channels (32-row blocks of 2 waves) on 64-wide maps -- the critic's 64-channel
+// stage, 64 -> 64 at 64x64: 79 -> 93 TF/s (B = 128); the 128-channel 32x32 stage and the 16-row
+// tiles ran slower that way (profiles/r05_ab_wrow.txt).
+bool all_rows(int M, int J, int W, int K) {
+  return GANAMD_WROW_ALLK && K == 3 && W == 64 && M > 48 && M <= 64 && J >= 32;
+}
 
-template <int MB, int NW, int TN, int KK, bool S>
+template <int MB, int NW, int TN, int KK, bool S, bool AK = false>
 hipError_t go(const Args& a, hipStream_t st) {
-  constexpr bool AK = all_rows(KK);
   const dim3 grid((a.J + TN * MB - 1) / (TN * MB), (a.M + NW * MB - 1) / (NW * MB), (AK ? 1 : KK) * a.splits);
   hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK>), grid, dim3(64 * NW), 0, st, a);
   return hipGetLastError();
@@ -447,7 +451,10 @@ hipError_t go_tile(const Args& a, hipStream_t st) {
   const Tile t = tile_of(a.M);
   if (t.mb == 16) return go<16, 3, 3, KK, S>(a, st);
   switch (t.nw) {
-    case 2: return go<32, 2, 1, KK, S>(a, st);
+    case 2:
+      if constexpr (KK == 3)
+        if (all_rows(a.M, a.J, a.W, KK)) return go<32, 2, 1, KK, S, true>(a, st);
+      return go<32, 2, 1, KK, S>(a, st);
     case 3: return go<32, 3, 1, KK, S>(a, st);
     case 4: return go<32, 4, 1, KK, S>(a, st);
     default: return hipErrorInvalidValue;
@@ -466,7 +473,7 @@ bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW, int
 void plan(int M, int J, int B, int H, int W, int K, int segs, int cus, int* splits, int* ks_per_split) {
   const Tile t = tile_of(M);
   const long tiles = (long)((J + t.tn * t.mb - 1) / (t.tn * t.mb)) * ((M + t.nw * t.mb - 1) / (t.nw * t.mb)) *
-                     (all_rows(K) ? 1 : K);
+                     (all_rows(M, J, W, K) ? 1 : K);
   const long ks_total = (long)segs * B * H * W / KS;
   const long target = 4L * cus;
   long s = std::max<long>(1, (target + tiles - 1) / tiles);

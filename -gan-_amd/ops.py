@@ -614,7 +614,7 @@ class PReLUBackwardX(Function):
         gy = _c(gy)
         C, L = _rows(x)
         gx = torch.empty_like(x)
-        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), None, 0, None, stream()), "prelu_bwd")
+        check(LIB.ganamd_prelu_bwd(ptr(gy), ptr(x), ptr(a), C, L, ptr(gx), None, 0, None, 0, stream()), "prelu_bwd")
         ctx.save_for_backward(gy, x, a)
         return gx
 

@@ -264,7 +264,7 @@ def _bn_bwd(gy, x, C, L, gamma, beta, alpha, mean, invstd, gg, gb, ga):
     gx = torch.empty_like(x)
     ws = workspace(LIB.ganamd_rowreduce_workspace(C, L), x.device)
     check(LIB.ganamd_bn_act_bwd(ptr(gy), ptr(x), C, L, ptr(gamma), ptr(beta), ptr(alpha), ptr(mean), ptr(invstd),
-                                ptr(gx), ptr(gg), ptr(gb), ptr(ga), 1, ptr(ws), stream()), "bn_act_bwd")
+                                ptr(gx), ptr(gg), ptr(gb), ptr(ga), 1, *_lib.ws(ws), stream()), "bn_act_bwd")
     return gx
 
 

@@ -243,3 +243,40 @@ def test_undersized_workspace_rejected():
     assert L.ganamd_mbstd_adjoint(f, f, 64, f, f, 64, 4, 8, 16, 2, 4, f, f, mb, st) == -1
     assert L.ganamd_image_batch(f, 2, 80, 80, None, f, f, 4, 64, f, f, 4, 64, f, f, f, f,
                                 L.ganamd_image_batch_workspace(2, 80, 64) - 1, st) == -1
+
+
+def test_python_call_sites_match_signatures():
+    """Every ``LIB.ganamd_*(...)`` call in the package passes as many arguments as its ctypes
+    signature declares (a ``*ws(...)`` / ``*wsarg(...)`` expansion counts as the two workspace
+    arguments, pointer and bytes) -- ctypes would only notice on the GPU, at call time."""
+    import ast
+    from gan_amd import _lib
+    files = [os.path.join(d, f) for d in (os.path.join(REPO, "-gan-_amd"), os.path.join(REPO, "tests"))
+             for f in sorted(os.listdir(d)) if f.endswith(".py")] + [os.path.join(REPO, "bench.py")]
+    bad = []
+    for path in files:
+        fn = os.path.relpath(path, REPO)
+        tree = ast.parse(open(path).read())
+        for node in ast.walk(tree):
+            if not (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute)
+                    and node.func.attr.startswith("ganamd_")):
+                continue
+            name = node.func.attr
+            if name not in _lib._SIGS:
+                bad.append(f"{fn}:{node.lineno} {name}: not in the binding")
+                continue
+            n = 0
+            for a in node.args:
+                if isinstance(a, ast.Starred):
+                    f = a.value.func if isinstance(a.value, ast.Call) else None
+                    fname = f.attr if isinstance(f, ast.Attribute) else getattr(f, "id", None)
+                    if fname not in ("ws", "wsarg"):      # another expansion (e.g. a padded pointer list)
+                        n = None
+                        break
+                    n += 2
+                else:
+                    n += 1
+            want = len(_lib._SIGS[name][1])
+            if n is not None and n != want:
+                bad.append(f"{fn}:{node.lineno} {name}: {n} arguments, signature has {want}")
+    assert not bad, bad
