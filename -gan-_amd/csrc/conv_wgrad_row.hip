@@ -42,6 +42,9 @@ constexpr int KS = 32;                 // output pixels per K-step (one row segm
 #ifndef GANAMD_WROW_ALLK
 #define GANAMD_WROW_ALLK 1             // 3x3: one block runs all three kernel rows on one staged A (all_rows)
 #endif
+#ifndef GANAMD_WROW_VMWAIT
+#define GANAMD_WROW_VMWAIT 1           // wait for every staged global load before the LDS stores (see vm_drain)
+#endif
 #ifndef GANAMD_WROW_APAD
 #define GANAMD_WROW_APAD 0             // bf16 elements between the two substeps' A planes (A/B builds)
 #endif
@@ -57,6 +60,15 @@ __device__ __forceinline__ float bload(rsrc_t r, int off) {
 __device__ __forceinline__ f32x4 bload4(rsrc_t r, int off) {
   asm("" : "+v"(off));
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their maxima): the staged registers are complete
+// before they are split and stored.  Without it some 16-lane groups of the scaled instances stored
+// values of an earlier K-step now and then (run-to-run different sums,
+// tests/test_ops_gpu.py::test_conv_wgrad_deterministic); the loads were issued before the
+// K-step's products, so the wait costs nothing measurable.
+__device__ __forceinline__ void vm_drain() {
+  if constexpr (GANAMD_WROW_VMWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 // exact 3-way split x = h + m + l (RNE; both differences exact in fp32)
@@ -117,7 +129,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // ALLK: the block owns ALL K kernel rows: per K-step the output-gradient tile A is staged once and
 // the K input rows it meets (ih = oh + kh - pad) one after another through the double-buffered B
 // stage -- K times the products per staged A (accumulators K * K per column block).
-template <int MB, int NW, int TN, int KK, bool SCALED, bool ALLK = false>
+template <int MB, int NW, int TN, int KK, bool SCALED, bool ALLK, bool REP>
 __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   constexpr int NT = 64 * NW, BM = NW * MB, BJ = TN * MB, PAD = (KK - 1) / 2, T = KK * KK;
   constexpr int SEG = KS + KK - 1;                 // staged input columns
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   auto bload_row = [&](const KStep& k, int kh, Stage& S) {
     int ih = k.oh + kh - PAD;
     bool row_in = true;
-    if (p.replicate)
+    if constexpr (REP)
       ih = min(max(ih, 0), p.H - 1);
     else
       row_in = ih >= 0 && ih < p.H;
@@ -205,7 +217,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
         const int c = 4 * cg + q;
         int iw = k.ow0 - PAD + c;
         bool in = row_in && j < p.J && c < SEG;
-        if (p.replicate)
+        if constexpr (REP)
           iw = min(max(iw, 0), W - 1);
         else
           in = in && iw >= 0 && iw < W;
@@ -216,6 +228,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   };
   // registers -> LDS (scaled, split into the three planes)
   auto astore = [&](int buf, const Stage& S) {
+    vm_drain();
 #pragma unroll
     for (int e = 0; e < AUT; ++e) {
       const int u = tid + e * NT;
@@ -240,6 +253,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     }
   };
   auto bstore = [&](int buf, const Stage& S) {
+    vm_drain();
 #pragma unroll
     for (int e = 0; e < BUT; ++e) {
       const int u = tid + e * NT;
@@ -442,7 +456,13 @@ bool all_rows(int M, int J, int W, int K) {
 template <int MB, int NW, int TN, int KK, bool S, bool AK = false>
 hipError_t go(const Args& a, hipStream_t st) {
   const dim3 grid((a.J + TN * MB - 1) / (TN * MB), (a.M + NW * MB - 1) / (NW * MB), (AK ? 1 : KK) * a.splits);
-  hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK>), grid, dim3(64 * NW), 0, st, a);
+  // the pad mode is a template argument: a run-time branch per staged column left the input-row
+  // loads in a web of small blocks whose compiled form gave run-to-run different sums (the 96-row
+  // 3x3 instance at 64x64, tests/test_ops_gpu.py::test_conv_wgrad_deterministic)
+  if (a.replicate)
+    hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK, true>), grid, dim3(64 * NW), 0, st, a);
+  else
+    hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK, false>), grid, dim3(64 * NW), 0, st, a);
   return hipGetLastError();
 }
 

@@ -887,6 +887,38 @@ def test_conv_wgrad_row(ops, case):
         assert rel(ops._conv_wgrad(geo, cn(x), cn(gy), f(sx), f(sy), 0.3), want) < 1e-5
 
 
+WGRAD_DET_CASES = WGRAD_ROW_CASES + [
+    # the generator's 96-channel 3x3 stage (SK conv_0, 32x32 and 64x64 maps) and its 96 -> 54 conv3
+    (8, 96, 32, 96, 3, 1, True), (8, 96, 64, 96, 3, 1, True), (8, 96, 64, 54, 3, 1, True),
+    (8, 96, 32, 96, 5, 1, True), (32, 64, 64, 64, 3, 1, False),
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_DET_CASES)
+def test_conv_wgrad_deterministic(ops, case):
+    """The weight gradient is a function of its inputs alone: four calls on the same operands, each
+    into a workspace the caching allocator hands back full of NaN, give the same bits (a partial sum
+    read before it is written, or a slab entry no block writes, shows up here as a changed result)."""
+    B, Cin, H, Cout, k, mode, scaled = case
+    p = (k - 1) // 2
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
+    g = torch.Generator(device=DEV).manual_seed(sum(case[:6]))
+    x = torch.randn(Cin, B, H, H, generator=g, device=DEV)
+    gy = torch.randn(Cout, B, H, H, generator=g, device=DEV)
+    sx = torch.rand(Cin, B, generator=g, device=DEV) + 0.5 if scaled else None
+    sy = torch.rand(Cout, B, generator=g, device=DEV) + 0.5 if scaled else None
+    nb = geo.ws_bytes(ops._lib.CONV_WGRAD)
+    outs = []
+    for _ in range(4):
+        junk = torch.full((max(nb, 4) // 4 + 1,), float("nan"), device=DEV)
+        del junk
+        outs.append(ops._conv_wgrad(geo, x, gy, sx, sy, 0.3))
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), float((o - outs[0]).abs().max())
+
+
 @pytest.mark.parametrize("B,cin,cout,H,k,aligned", [(4, 48, 54, 16, 3, True), (3, 20, 12, 8, 5, True),
                                                     (2, 6, 5, 5, 3, False)])
 def test_modconv_noise_grads(ops, B, cin, cout, H, k, aligned):
