@@ -39,15 +39,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kOOB = (int)0x80000000;
 constexpr int KS = 32;                 // output pixels per K-step (one row segment: W % 32 == 0)
-#ifndef GANAMD_WROW_ALLK
-#define GANAMD_WROW_ALLK 1             // 3x3: one block runs all three kernel rows on one staged A (all_rows)
-#endif
-#ifndef GANAMD_WROW_VMWAIT
-#define GANAMD_WROW_VMWAIT 1           // wait for every staged global load before the LDS stores (see vm_drain)
-#endif
-#ifndef GANAMD_WROW_APAD
-#define GANAMD_WROW_APAD 0             // bf16 elements between the two substeps' A planes (A/B builds)
-#endif
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)std::min<long>(bytes, 0x7fffffff),
@@ -60,15 +51,6 @@ __device__ __forceinline__ float bload(rsrc_t r, int off) {
 __device__ __forceinline__ f32x4 bload4(rsrc_t r, int off) {
   asm("" : "+v"(off));
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their maxima): the staged registers are complete
-// before they are split and stored.  Without it some 16-lane groups of the scaled instances stored
-// values of an earlier K-step now and then (run-to-run different sums,
-// tests/test_ops_gpu.py::test_conv_wgrad_deterministic); the loads were issued before the
-// K-step's products, so the wait costs nothing measurable.
-__device__ __forceinline__ void vm_drain() {
-  if constexpr (GANAMD_WROW_VMWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 // exact 3-way split x = h + m + l (RNE; both differences exact in fp32)
@@ -126,20 +108,14 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// ALLK: the block owns ALL K kernel rows: per K-step the output-gradient tile A is staged once and
-// the K input rows it meets (ih = oh + kh - pad) one after another through the double-buffered B
-// stage -- K times the products per staged A (accumulators K * K per column block).
-template <int MB, int NW, int TN, int KK, bool SCALED, bool ALLK, bool REP>
+template <int MB, int NW, int TN, int KK, bool SCALED>
 __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   constexpr int NT = 64 * NW, BM = NW * MB, BJ = TN * MB, PAD = (KK - 1) / 2, T = KK * KK;
   constexpr int SEG = KS + KK - 1;                 // staged input columns
   // B row stride (bf16): 112 B (7 16-byte chunks) for 32-row blocks, 96 B (6 chunks) for 16-row
   // blocks -- the row strides whose window reads are conflict-free for each fragment's lane groups
   constexpr int LDB = MB == 32 ? 56 : 48;
-  // two 16-pixel substeps x three planes; the second substep's planes start GANAMD_WROW_APAD bf16
-  // further: at 3 * PSA = a multiple of 256 bytes the A stores of units g and g + 2 (same row, the two
-  // substeps) hit the same banks (ds_write_b128: 8 lanes = two rows x four units per LDS cycle)
-  constexpr int PSA = BM * 16, SSA = 3 * PSA + GANAMD_WROW_APAD, ABUF = 2 * SSA;
+  constexpr int PSA = BM * 16, ABUF = 2 * 3 * PSA; // two 16-pixel substeps x three planes
   constexpr int PSB = BJ * LDB, BBUF = 3 * PSB;
   constexpr int AU = BM * 4, AUT = (AU + NT - 1) / NT;   // A units: 8 pixels of one row
   constexpr int BU = BJ * 12, BUT = (BU + NT - 1) / NT;  // B units: 4 columns of one row (48 staged)
@@ -150,8 +126,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j0 = blockIdx.x * BJ, m0 = blockIdx.y * BM;
-  const int kh_blk = ALLK ? 0 : blockIdx.z / p.splits, split = ALLK ? blockIdx.z : blockIdx.z - kh_blk * p.splits;
-  constexpr int NKH = ALLK ? KK : 1;                 // kernel rows this block accumulates
+  const int kh = blockIdx.z / p.splits, split = blockIdx.z - kh * p.splits;
   const int W = p.W, HW = p.H * W;
   const long L = (long)p.B * HW;                   // row length of a / x
   const int ks_seg = (int)(L / KS);
@@ -169,41 +144,26 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     f32x4 rb[BUT];
     float sa[AUT], sb[BUT];
   };
-  struct KStep {                                   // where K-step ks reads
-    rsrc_t ra, rx;
-    long n0;
-    int b, oh, ow0;
-  };
-  auto kstep = [&](int ks) {
+  // global -> registers for K-step ks
+  auto gload = [&](int ks, Stage& S) {
     const bool s2 = ks >= ks_seg;
     const int kl = s2 ? ks - ks_seg : ks;
-    KStep k;
-    k.ra = s2 ? ra2 : ra1;
-    k.rx = s2 ? rx2 : rx1;
-    k.n0 = (long)kl * KS;
-    k.b = (int)(k.n0 / HW);
-    const int rem = (int)(k.n0 - (long)k.b * HW);
-    k.oh = rem / W;
-    k.ow0 = rem - k.oh * W;
-    return k;
-  };
-  // global -> registers: the A tile of K-step k ...
-  auto aload = [&](const KStep& k, Stage& S) {
+    const rsrc_t ra = s2 ? ra2 : ra1, rx = s2 ? rx2 : rx1;
+    const long n0 = (long)kl * KS;
+    const int b = (int)(n0 / HW), rem = (int)(n0 - (long)b * HW);
+    const int oh = rem / W, ow0 = rem - oh * W;
 #pragma unroll
     for (int e = 0; e < AUT; ++e) {
       const int u = min(tid + e * NT, AU - 1), r = u >> 2, g = u & 3;
       const int m = m0 + r;
-      const int off = m < p.M ? (int)(4 * ((long)m * L + k.n0 + 8 * g)) : kOOB;
-      S.ra[e][0] = bload4(k.ra, off);
-      S.ra[e][1] = bload4(k.ra, off == kOOB ? kOOB : off + 16);
-      if (SCALED) S.sa[e] = bload(rsa, m < p.M ? 4 * (m * p.B + k.b) : kOOB);
+      const int off = m < p.M ? (int)(4 * ((long)m * L + n0 + 8 * g)) : kOOB;
+      S.ra[e][0] = bload4(ra, off);
+      S.ra[e][1] = bload4(ra, off == kOOB ? kOOB : off + 16);
+      if (SCALED) S.sa[e] = bload(rsa, m < p.M ? 4 * (m * p.B + b) : kOOB);
     }
-  };
-  // ... and its input row segment for kernel row kh
-  auto bload_row = [&](const KStep& k, int kh, Stage& S) {
-    int ih = k.oh + kh - PAD;
+    int ih = oh + kh - PAD;
     bool row_in = true;
-    if constexpr (REP)
+    if (p.replicate)
       ih = min(max(ih, 0), p.H - 1);
     else
       row_in = ih >= 0 && ih < p.H;
@@ -211,24 +171,23 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     for (int e = 0; e < BUT; ++e) {
       const int u = min(tid + e * NT, BU - 1), jr = u / 12, cg = u - jr * 12;
       const int j = j0 + jr;
-      const long rowbase = (long)j * L + (long)k.b * HW + (long)ih * W;
+      const long rowbase = (long)j * L + (long)b * HW + (long)ih * W;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = 4 * cg + q;
-        int iw = k.ow0 - PAD + c;
+        int iw = ow0 - PAD + c;
         bool in = row_in && j < p.J && c < SEG;
-        if constexpr (REP)
+        if (p.replicate)
           iw = min(max(iw, 0), W - 1);
         else
           in = in && iw >= 0 && iw < W;
-        S.rb[e][q] = bload(k.rx, in ? (int)(4 * (rowbase + iw)) : kOOB);
+        S.rb[e][q] = bload(rx, in ? (int)(4 * (rowbase + iw)) : kOOB);
       }
-      if (SCALED) S.sb[e] = bload(rsx, j < p.J ? 4 * (j * p.B + k.b) : kOOB);
+      if (SCALED) S.sb[e] = bload(rsx, j < p.J ? 4 * (j * p.B + b) : kOOB);
     }
   };
   // registers -> LDS (scaled, split into the three planes)
-  auto astore = [&](int buf, const Stage& S) {
-    vm_drain();
+  auto sstore = [&](int buf, const Stage& S) {
 #pragma unroll
     for (int e = 0; e < AUT; ++e) {
       const int u = tid + e * NT;
@@ -245,15 +204,12 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
           for (int q = 0; q < 8; ++q) v[q] *= S.sa[e];
         bf16x8 h, m, l;
         split3<8>(v, h, m, l);
-        unsigned short* d = &As[buf][(g >> 1) * SSA + aoff<MB>(r, g & 1)];
+        unsigned short* d = &As[buf][(g >> 1) * 3 * PSA + aoff<MB>(r, g & 1)];
         *reinterpret_cast<bf16x8*>(d) = h;
         *reinterpret_cast<bf16x8*>(d + PSA) = m;
         *reinterpret_cast<bf16x8*>(d + 2 * PSA) = l;
       }
     }
-  };
-  auto bstore = [&](int buf, const Stage& S) {
-    vm_drain();
 #pragma unroll
     for (int e = 0; e < BUT; ++e) {
       const int u = tid + e * NT;
@@ -273,15 +229,13 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
     }
   };
 
-  acc_t acc[NKH][TN][KK];
+  acc_t acc[TN][KK];
 #pragma unroll
-  for (int q = 0; q < NKH; ++q)
+  for (int jb = 0; jb < TN; ++jb)
 #pragma unroll
-    for (int jb = 0; jb < TN; ++jb)
+    for (int t = 0; t < KK; ++t)
 #pragma unroll
-      for (int t = 0; t < KK; ++t)
-#pragma unroll
-        for (int r = 0; r < NR; ++r) acc[q][jb][t][r] = 0.f;
+      for (int r = 0; r < NR; ++r) acc[jb][t][r] = 0.f;
 
   // lane roles: 32x32 -- (r, h): A row r, k = 8h..8h+7; B column r.  16x16 paired -- (r, q):
   // half hf = q & 1 (k = 8hf..), pair hi = q >> 1: A (h|m), (h|l), (m|h); B (h|h), (m|h), (m|l)
@@ -289,13 +243,10 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   const int fh = MB == 32 ? (lane >> 5) : ((lane >> 4) & 1);
   const int hi = MB == 32 ? 0 : (lane >> 5);
   const int arow = wv * MB + fr;
-  // the products of the staged A (buffer abuf) with the staged input row (buffer bbuf) into the
-  // accumulators of kernel row QK
-  auto compute = [&](int abuf, int bbuf, auto QKc) {
-    constexpr int QK = decltype(QKc)::value;
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {                      // two 16-pixel substeps
-      const unsigned short* A = &As[abuf][s * SSA + aoff<MB>(arow, fh)];
+      const unsigned short* A = &As[buf][s * 3 * PSA + aoff<MB>(arow, fh)];
       bf16x8 a[3];
       if constexpr (MB == 32) {
 #pragma unroll
@@ -307,7 +258,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
       }
 #pragma unroll
       for (int jb = 0; jb < TN; ++jb) {
-        const unsigned short* Bp = &Bs[bbuf][(jb * MB + fr) * LDB + 16 * s + 8 * fh];
+        const unsigned short* Bp = &Bs[buf][(jb * MB + fr) * LDB + 16 * s + 8 * fh];
         if constexpr (MB == 32) {
           u32x4 w[3][2];
 #pragma unroll
@@ -319,7 +270,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
             constexpr int kw = decltype(KWc)::value;
             const bf16x8 bh = shifted<kw>(w[0][0], w[0][1]), bm = shifted<kw>(w[1][0], w[1][1]),
                          bl = shifted<kw>(w[2][0], w[2][1]);
-            acc_t& c = acc[QK][jb][kw];
+            acc_t& c = acc[jb][kw];
             // l*h, h*l, m*m, m*h, h*m, h*h: smallest first into the same accumulator
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bh, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bl, c, 0, 0, 0);
@@ -336,7 +287,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
           static_for<0, KK>([&](auto KWc) {
             constexpr int kw = decltype(KWc)::value;
             const bf16x8 bh = shifted<kw>(wh0, wh1), bx = shifted<kw>(wx0, wx1);
-            acc_t& c = acc[QK][jb][kw];
+            acc_t& c = acc[jb][kw];
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bh, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], hi ? bh : bx, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bx, c, 0, 0, 0);
@@ -347,90 +298,40 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
   };
 
   if (k0 < k1) {
-    if constexpr (!ALLK) {
-      Stage s0;
-      {
-        const KStep k = kstep(k0);
-        aload(k, s0);
-        bload_row(k, kh_blk, s0);
-      }
-      astore(0, s0);
-      bstore(0, s0);
+    Stage s0;
+    gload(k0, s0);
+    sstore(0, s0);
+    __syncthreads();
+    for (int ks = k0; ks < k1; ++ks) {
+      const int buf = (ks - k0) & 1;
+      const bool more = ks + 1 < k1;
+      if (more) gload(ks + 1, s0);
+      compute(buf);
+      if (more) sstore(buf ^ 1, s0);
       __syncthreads();
-      for (int ks = k0; ks < k1; ++ks) {
-        const int buf = (ks - k0) & 1;
-        const bool more = ks + 1 < k1;
-        if (more) {
-          const KStep k = kstep(ks + 1);
-          aload(k, s0);
-          bload_row(k, kh_blk, s0);
-        }
-        compute(buf, buf, std::integral_constant<int, 0>{});
-        if (more) {
-          astore(buf ^ 1, s0);
-          bstore(buf ^ 1, s0);
-        }
-        __syncthreads();
-      }
-    } else {
-      // units u = (ks, kh) in order; A double-buffered per K-step, B per unit
-      Stage s0;
-      KStep k = kstep(k0);
-      aload(k, s0);
-      bload_row(k, 0, s0);
-      astore(0, s0);
-      bstore(0, s0);
-      __syncthreads();
-      int bb = 0;
-      for (int ks = k0; ks < k1; ++ks) {
-        const int ab = (ks - k0) & 1;
-        const bool more = ks + 1 < k1;
-        static_for<0, KK>([&](auto QKc) {
-          constexpr int kh = decltype(QKc)::value;
-          const bool next = kh + 1 < KK || more;        // a unit after this one
-          if (kh + 1 < KK) {
-            bload_row(k, kh + 1, s0);
-          } else if (more) {
-            k = kstep(ks + 1);
-            aload(k, s0);
-            bload_row(k, 0, s0);
-          }
-          compute(ab, bb, QKc);
-          if (next) {
-            bstore(bb ^ 1, s0);
-            if (kh + 1 == KK) astore(ab ^ 1, s0);
-          }
-          __syncthreads();
-          bb ^= 1;
-        });
-      }
     }
   }
 
   // epilogue: every block writes its whole tile (zeros for an empty K range)
   const long numel = (long)p.M * p.J * T;
 #pragma unroll
-  for (int q = 0; q < NKH; ++q) {
-    const int kh = ALLK ? q : kh_blk;
+  for (int jb = 0; jb < TN; ++jb) {
+    const int j = j0 + jb * MB + (lane & (MB - 1));
+    if (j >= p.J) continue;
 #pragma unroll
-    for (int jb = 0; jb < TN; ++jb) {
-      const int j = j0 + jb * MB + (lane & (MB - 1));
-      if (j >= p.J) continue;
+    for (int kw = 0; kw < KK; ++kw) {
 #pragma unroll
-      for (int kw = 0; kw < KK; ++kw) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          const int m = m0 + wv * MB + mfma_row<MB>(lane, r);
-          if (m >= p.M) continue;
-          const long o = ((long)m * p.J + j) * T + kh * KK + kw;
-          const float v = p.alpha * acc[q][jb][kw][r];
-          if (p.slab)
-            p.slab[(long)split * numel + o] = v;
-          else if (p.accumulate)
-            p.out[o] += v;
-          else
-            p.out[o] = v;
-        }
+      for (int r = 0; r < NR; ++r) {
+        const int m = m0 + wv * MB + mfma_row<MB>(lane, r);
+        if (m >= p.M) continue;
+        const long o = ((long)m * p.J + j) * T + kh * KK + kw;
+        const float v = p.alpha * acc[jb][kw][r];
+        if (p.slab)
+          p.slab[(long)split * numel + o] = v;
+        else if (p.accumulate)
+          p.out[o] += v;
+        else
+          p.out[o] = v;
       }
     }
   }
@@ -445,24 +346,10 @@ Tile tile_of(int M) {
   return {32, (M + 31) / 32, 1};
 }
 
-// Whether a launch runs all kernel rows per block (a function of the geometry alone): the 3x3 weight
-// gradients of 64 output channels (32-row blocks of 2 waves) on 64-wide maps -- the critic's 64-channel
-// stage, 64 -> 64 at 64x64: 79 -> 93 TF/s (B = 128); the 128-channel 32x32 stage and the 16-row
-// tiles ran slower that way (profiles/r05_ab_wrow.txt).
-bool all_rows(int M, int J, int W, int K) {
-  return GANAMD_WROW_ALLK && K == 3 && W == 64 && M > 48 && M <= 64 && J >= 32;
-}
-
-template <int MB, int NW, int TN, int KK, bool S, bool AK = false>
+template <int MB, int NW, int TN, int KK, bool S>
 hipError_t go(const Args& a, hipStream_t st) {
-  const dim3 grid((a.J + TN * MB - 1) / (TN * MB), (a.M + NW * MB - 1) / (NW * MB), (AK ? 1 : KK) * a.splits);
-  // the pad mode is a template argument: a run-time branch per staged column left the input-row
-  // loads in a web of small blocks whose compiled form gave run-to-run different sums (the 96-row
-  // 3x3 instance at 64x64, tests/test_ops_gpu.py::test_conv_wgrad_deterministic)
-  if (a.replicate)
-    hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK, true>), grid, dim3(64 * NW), 0, st, a);
-  else
-    hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S, AK, false>), grid, dim3(64 * NW), 0, st, a);
+  const dim3 grid((a.J + TN * MB - 1) / (TN * MB), (a.M + NW * MB - 1) / (NW * MB), KK * a.splits);
+  hipLaunchKernelGGL((wgrad_row_kernel<MB, NW, TN, KK, S>), grid, dim3(64 * NW), 0, st, a);
   return hipGetLastError();
 }
 
@@ -471,10 +358,7 @@ hipError_t go_tile(const Args& a, hipStream_t st) {
   const Tile t = tile_of(a.M);
   if (t.mb == 16) return go<16, 3, 3, KK, S>(a, st);
   switch (t.nw) {
-    case 2:
-      if constexpr (KK == 3)
-        if (all_rows(a.M, a.J, a.W, KK)) return go<32, 2, 1, KK, S, true>(a, st);
-      return go<32, 2, 1, KK, S>(a, st);
+    case 2: return go<32, 2, 1, KK, S>(a, st);
     case 3: return go<32, 3, 1, KK, S>(a, st);
     case 4: return go<32, 4, 1, KK, S>(a, st);
     default: return hipErrorInvalidValue;
@@ -492,8 +376,7 @@ bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW, int
 // CU), each split at least 16 K-steps (512 pixels).
 void plan(int M, int J, int B, int H, int W, int K, int segs, int cus, int* splits, int* ks_per_split) {
   const Tile t = tile_of(M);
-  const long tiles = (long)((J + t.tn * t.mb - 1) / (t.tn * t.mb)) * ((M + t.nw * t.mb - 1) / (t.nw * t.mb)) *
-                     (all_rows(M, J, W, K) ? 1 : K);
+  const long tiles = (long)((J + t.tn * t.mb - 1) / (t.tn * t.mb)) * ((M + t.nw * t.mb - 1) / (t.nw * t.mb)) * K;
   const long ks_total = (long)segs * B * H * W / KS;
   const long target = 4L * cus;
   long s = std::max<long>(1, (target + tiles - 1) / tiles);

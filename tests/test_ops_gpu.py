@@ -896,7 +896,7 @@ WGRAD_DET_CASES = WGRAD_ROW_CASES + [
 
 @pytest.mark.parametrize("case", WGRAD_DET_CASES)
 def test_conv_wgrad_deterministic(ops, case):
-    """The weight gradient is a function of its inputs alone: four calls on the same operands, each
+    """The weight gradient is a function of its inputs alone: eight calls on the same operands, each
     into a workspace the caching allocator hands back full of NaN, give the same bits (a partial sum
     read before it is written, or a slab entry no block writes, shows up here as a changed result)."""
     B, Cin, H, Cout, k, mode, scaled = case
@@ -909,7 +909,7 @@ def test_conv_wgrad_deterministic(ops, case):
     sy = torch.rand(Cout, B, generator=g, device=DEV) + 0.5 if scaled else None
     nb = geo.ws_bytes(ops._lib.CONV_WGRAD)
     outs = []
-    for _ in range(4):
+    for _ in range(8):
         junk = torch.full((max(nb, 4) // 4 + 1,), float("nan"), device=DEV)
         del junk
         outs.append(ops._conv_wgrad(geo, x, gy, sx, sy, 0.3))
