@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import weakref
 
 from dataclasses import dataclass
 
@@ -259,11 +260,14 @@ class PackCache:
         key = base_key + (cap,)
         epoch = (id(flat), flat.epoch) if flat is not None else cls.epoch
         e = cls.entries.get(key)
-        if e is not None and e[0] is root and e[1] == root._version and e[2] == epoch:
+        if e is not None and e[0]() is root and e[1] == root._version and e[2] == epoch:
             return e[3]
         packed = cls._alloc(geo, op, w)
         cls._pack(geo, op, w, packed)
-        cls.entries[key] = (root, root._version, epoch, packed)
+        # the weight is held weakly and its copies leave with it: a process that builds model after
+        # model (the GPU test suite: 25 GB of packed copies of dead models) keeps only live ones
+        entries = cls.entries
+        cls.entries[key] = (weakref.ref(root, lambda _r, k=key: entries.pop(k, None)), root._version, epoch, packed)
         return packed
 
 

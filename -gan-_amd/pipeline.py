@@ -30,6 +30,8 @@ optimizer graph (collectives stay outside capture).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .dist import allreduce_mean_
@@ -95,9 +97,18 @@ class Iteration:
         with torch.cuda.stream(s):          # one eager run on a side stream (allocator warm-up)
             fn()
         torch.cuda.current_stream().wait_stream(s)
+        # the warm-up's blocks are cached against the throw-away stream s, where nothing can reuse
+        # them: hand them back before the capture fills its pool (without this every phase graph
+        # left its eager peak behind)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=pool):
             fn()
+        if os.environ.get("DP_MEMLOG") == "1":
+            torch.cuda.synchronize()
+            print(f"[mem] captured {getattr(fn, '__name__', fn)}: allocated {torch.cuda.memory_allocated() / 2**30:.1f} "
+                  f"GiB, reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB", flush=True)
         return g
 
     def capture(self):
@@ -209,8 +220,9 @@ def training_state(tr):
     return ts
 
 
-def snapshot(tr):
-    st = [t.detach().clone() for t in training_state(tr)]
+def snapshot(tr, device=None):
+    """The training state (``device``: where the copies live, default alongside the originals)."""
+    st = [t.detach().to(device, copy=True) if device is not None else t.detach().clone() for t in training_state(tr)]
     rng = tr.rng.state() if hasattr(tr.rng, "state") else None
     return st, rng
 

@@ -100,6 +100,14 @@ class FirstAllreduce:
         return flat
 
 
+def _mem(tag):
+    if os.environ.get("DP_MEMLOG") == "1":
+        torch.cuda.synchronize()
+        print(f"[mem] {tag}: allocated {torch.cuda.memory_allocated() / 2**30:.1f} GiB, reserved "
+              f"{torch.cuda.memory_reserved() / 2**30:.1f} GiB, peak {torch.cuda.max_memory_reserved() / 2**30:.1f}",
+              flush=True)
+
+
 def main_graph(out):
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
@@ -115,9 +123,19 @@ def main_graph(out):
     bs = int(sys.argv[4]) if len(sys.argv) > 4 else B_GRAPH
     ar = FirstAllreduce()
     it = Iteration(tr, bs, 5, world, overlap=not serial, fake_groups=GRAPH_FAKE_GROUPS, allreduce=ar)
-    snap = snapshot(tr)
+    snap = snapshot(tr, "cpu")     # two B = 64 ranks and the test share one GPU: host copies
+    _mem("models")
     it.eager()                     # warm-up (all-reduces included), then capture
-    it.capture()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    _mem("eager warm-up")
+    # the ranks capture one after another: both share one GPU here, and a capture peaks at the
+    # graph pools plus one phase's eager warm-up (~140 GB per rank at B = 64)
+    for r in range(world):
+        if r == rank:
+            it.capture()
+        dist.barrier()
+    _mem("captured")
     restore(tr, snap)
     dist.barrier()
     ar.armed = True
@@ -127,7 +145,8 @@ def main_graph(out):
            (("g_data", tr.optimizer_G.flat.data), ("g_grad", tr.optimizer_G.flat.grad),
             ("d_data", tr.optimizer_D.flat.data), ("d_grad", tr.optimizer_D.flat.grad))}
     if rank == 0:
-        torch.save(dict(res, world=world, d_grad0=ar.first, batch=bs), out)
+        torch.save(dict(res, world=world, d_grad0=ar.first, batch=bs, peak_reserved=torch.cuda.max_memory_reserved(),
+                        reserved=torch.cuda.memory_reserved()), out)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -105,6 +105,23 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule, B):
     import gc
     gc.collect()
     torch.cuda.empty_cache()           # two B = 64 ranks share this GPU with this process's cache
+    free, total = torch.cuda.mem_get_info()
+    print(f"before the ranks: {free / 2**30:.1f} of {total / 2**30:.1f} GiB free, this process reserves "
+          f"{torch.cuda.memory_reserved() / 2**30:.1f} GiB ({torch.cuda.memory_allocated() / 2**30:.1f} allocated)")
+    if os.environ.get("DP_MEMLOG") == "1":
+        big = sorted(((o.numel() * o.element_size(), tuple(o.shape)) for o in gc.get_objects()
+                      if torch.is_tensor(o) and o.is_cuda), reverse=True)[:15]
+        print("largest live tensors:", [(round(n / 2**30, 2), s) for n, s in big])
+        top = [o for o in gc.get_objects() if torch.is_tensor(o) and o.is_cuda and o.numel() == big[0][1][0]][:3]
+        for t in top:
+            for r in gc.get_referrers(t):
+                desc = type(r).__name__
+                if isinstance(r, dict):
+                    desc += " keys " + str([k for k, v in r.items() if v is t][:3]) + " of " + str(list(r.keys())[:6])
+                elif isinstance(r, (list, tuple)):
+                    owners = [type(q).__name__ for q in gc.get_referrers(r)][:4]
+                    desc += f" len {len(r)} held by {owners}"
+                print("  referrer:", desc[:300])
     out = str(tmp_path / "rank0_graph.pt")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
@@ -113,6 +130,7 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule, B):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = torch.load(out, weights_only=True)
     assert got["world"] == 2 and got["batch"] == B and got["d_grad0"] is not None
+    print(f"rank 0: peak {got['peak_reserved'] / 2**30:.1f} GiB reserved, {got['reserved'] / 2**30:.1f} GiB at the end")
 
     import gan_amd
     dev = torch.device("cuda", 0)
