@@ -1609,23 +1609,17 @@ double list_makespan(long F, double L, long R, double d, long slots) {
 constexpr double kSustainedTflops = 150.0;   // chip-wide fp32 rate of the GEMM body (split6), all slots busy
 constexpr double kSustainedTflopsBf16 = 300.0;   // the bf16-LDS body (conv_body_bf16), gather-bound
 
-ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {
+// The plan of one tile shape (bm x bn) and its modelled makespan in microseconds.
+static ConvPlan conv_plan_tile(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16, int bm, int bn,
+                               double rate, double* cost_us) {
   ConvPlan pl{};
-  conv_tile(M, &pl.bm, &pl.bn);
-  pl.bn = conv_bn(pl.bm, bscale, bf16);
-  // the bf16 body has 32x32 blocks only: its 48-row GEMMs run on the 64-row tile over the same
-  // 48-row packed operand (rows past it read as 0 through the buffer bound, are not stored)
-  if (bf16 && pl.bm == 48) {
-    pl.bm = 64;
-    pl.bn = conv_bn(64, bscale, bf16);
-  }
-  if (bf16 && pl.bm == 16) pl.bm = 32;
+  pl.bm = bm;
+  pl.bn = bn;
   pl.gx = (N + pl.bn - 1) / pl.bn;
   pl.gy = (M + pl.bm - 1) / pl.bm;
   // bf16 kernels take K-steps of BKB = two fp32 steps (conv_body_bf16)
   const int kt_total = bf16 ? (((Ck + BK - 1) / BK) * T + 1) / 2 : ((Ck + BK - 1) / BK) * T;
   const int bk = bf16 ? BKB : BK;
-  const double rate = bf16 ? kSustainedTflopsBf16 : kSustainedTflops;
   const long tiles = (long)pl.gx * pl.gy;
   // slot-level model (blocks run in rounds of occupancy x CUs); the CU-level "fluid" model was
   // measured 7 % slower over the iteration (it under-splits: a lone block does not fill its CU)
@@ -1668,6 +1662,33 @@ ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16
   pl.S = (kt_total + pp - 1) / pp;
   const long tail_cols = std::max<long>(0, N - (long)pl.nfull_t * pl.bn);
   pl.slab_elems = (pl.S > 1 && tail_cols > 0) ? (long)pl.S * M * tail_cols : 0;
+  *cost_us = best * t_k;
+  return pl;
+}
+
+// 128x256 tiles (2 waves/SIMD) over 128x128 (3 waves/SIMD): per FLOP the wide tile is faster
+// when the chip is full (128 -> 128 3x3 32x32 at B = 128: 246 -> 213 us), but it halves the tile
+// count, so a grid that fills the narrow tile's slots in whole rounds leaves the wide tile's
+// slots a round and a half (B = 96: 179 -> 203 us).  Both plans are costed; the wide one carries
+// this measured per-FLOP gain (profiles/r05_ab_wide.txt).
+constexpr double kWideGain = 1.14;
+
+ConvPlan conv_plan(int M, int N, int Ck, int T, int mode, bool bscale, bool bf16) {
+  int bm, bn;
+  conv_tile(M, &bm, &bn);
+  bn = (bm <= 32) ? 256 : 128;
+  // the bf16 body has 32x32 blocks only: its 48-row GEMMs run on the 64-row tile over the same
+  // 48-row packed operand (rows past it read as 0 through the buffer bound, are not stored)
+  if (bf16 && bm == 48) bm = 64;
+  if (bf16 && bm == 16) bm = 32;
+  const double rate = bf16 ? kSustainedTflopsBf16 : kSustainedTflops;
+  double c0 = 0.0;
+  ConvPlan pl = conv_plan_tile(M, N, Ck, T, mode, bscale, bf16, bm, bn, rate, &c0);
+  if (conv_bn(bm, bscale, bf16) == 256 && bn != 256) {
+    double c1 = 0.0;
+    const ConvPlan w = conv_plan_tile(M, N, Ck, T, mode, bscale, bf16, bm, 256, rate * kWideGain, &c1);
+    if (c1 < c0) pl = w;
+  }
   return pl;
 }
 

@@ -37,6 +37,10 @@ SHAPES_DG = [   # fwd vs dgrad vs wgrad of the same critic convs (AB_SET=dg)
     ("fwd", 64, 256, 16, 256, 3, 1, 1, False, 55),
     ("dgrad", 64, 256, 16, 256, 3, 1, 1, False, 55),
 ]
+SHAPES_WIDE = [    # unscaled critic GEMMs across the batches the step runs them at (AB_SET=wide)
+    *[(op, b, c, h, c, 3, 1, 1, False, 1) for op in ("fwd", "dgrad")
+      for c, h in ((64, 64), (128, 32), (256, 16), (512, 8)) for b in (32, 64, 96, 128)],
+]
 SHAPES_PATCH = [   # the LDS-patch conv's instances (AB_SET=patch)
     ("fwd", 64, 96, 64, 96, 5, 1, 2, True, 30),
     ("fwd", 256, 96, 64, 96, 5, 1, 2, True, 10),
@@ -115,7 +119,7 @@ def child():
     from gan_amd import ops
     dev = torch.device("cuda")
     tot_t = tot_f = 0.0
-    for op, B, cin, H, cout, k, s, p, scaled, n in {"wgrad": SHAPES_WGRAD, "dg": SHAPES_DG, "patch": SHAPES_PATCH}.get(_os.environ.get("AB_SET"), SHAPES):
+    for op, B, cin, H, cout, k, s, p, scaled, n in {"wgrad": SHAPES_WGRAD, "dg": SHAPES_DG, "patch": SHAPES_PATCH, "wide": SHAPES_WIDE}.get(_os.environ.get("AB_SET"), SHAPES):
         g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
         x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
         y = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
