@@ -191,14 +191,15 @@ def cpu_baseline(threads, B=8):
 # rocprofv3 kernel trace reports; back-to-back launches also give the sustained rate):
 #   probe     D9_4's mid-level block conv, 128->128 channels, 3x3 replication pad, 32x32, at
 #             B = 96: 768 output tiles = one round of the kernel's resident blocks, so it is ONE
-#             launch of the critic's gather GEMM conv_gemm_kernel<128,128,2,2,1,false,false> --
-#             the top kernel INSTANCE of the iteration trace (profiles/r04_iteration_summary.txt:
-#             0.124 s over 1,020 launches of many shapes);
+#             launch of the critic's gather GEMM conv_gemm_kernel<128,128,2,2,1,false,false> (the
+#             plan keeps the 128x128 tile at this batch: the 128x256 one would leave 1.5 rounds);
 #   dominant  G13_5's 96-channel 5x5 modulated conv at 64x64 (x*s on the patch, *d in the
 #             epilogue), B = 64: one launch of the split6 LDS-patch conv conv_patch_x3_kernel<96,...>
-#             -- the top kernel FAMILY (the patch conv: 0.58 s of the iteration's 1.89 s busy) and
-#             the top single shape (0.110 s over 30 launches).  The line carries both; `top_instance`
-#             says which of them leads the committed trace by instance.
+#             -- the top kernel FAMILY (the patch conv: 0.54 s of the iteration's 1.80 s busy), the
+#             top single shape and, since round 5, the top kernel INSTANCE of the iteration trace
+#             (profiles/r05_iteration_summary.txt: 0.107 s over 30 launches; round 4's top instance
+#             was the critic GEMM, now split between its 128x128 and 128x256 forms).  `top_instance`
+#             records which kernel leads the committed trace by instance.
 PROBES = {
     "probe": dict(B=96, cin=128, h=32, cout=128, k=3, scaled=False,
                   shape="conv fwd B=96 128->128 3x3 replicate-pad 32x32 (D9_4 block conv; 768 whole tiles, one launch)"),
@@ -272,9 +273,9 @@ def probe_kernel(dev, spec, reps=20):
 
 # Which probed kernel leads the committed iteration trace by instance (kernel name with template
 # arguments; tools/trace_summary.py), and by family -- from the profile of this round's build.
-TOP_INSTANCE = {"kernel": "conv_gemm_kernel<128, 128, 2, 2, 1, false, false>", "probe": "critic_probe",
-                "iteration_s": 0.124, "launches": 1020, "family_top": "ganamd_patch::conv_patch_x3_kernel",
-                "family_s": 0.581, "source": "profiles/r04_iteration_summary.txt"}
+TOP_INSTANCE = {"kernel": "conv_patch_x3_kernel<96, 12, 512, 5, 64, true, false>", "probe": "dominant",
+                "iteration_s": 0.107, "launches": 30, "family_top": "ganamd_patch::conv_patch_x3_kernel",
+                "family_s": 0.538, "source": "profiles/r05_iteration_summary.txt"}
 
 
 def roofline_probe(dev):
