@@ -15,6 +15,7 @@ follows it, and Smooth / bicubic / adaptive pooling are tap-table resamples.
 from __future__ import annotations
 
 import math
+import os
 from typing import List
 
 import torch
@@ -22,6 +23,9 @@ from torch import nn
 
 from . import ops
 from .ops import bn_act, prelu
+
+# A/B: GANAMD_SHORTCUT_BRANCH=0 runs a root BasicBlock's shortcut after rir_3 instead of beside it
+SHORTCUT_BRANCH = [os.environ.get("GANAMD_SHORTCUT_BRANCH", "1") != "0"]
 
 
 def _normal(shape):
@@ -355,12 +359,15 @@ class ResnetInit(nn.Module):
         self.activation_residual = nn.PReLU(out_planes + dense_depth)
         self.activation_transient = nn.PReLU(out_planes)
 
-    def forward(self, x, w):
+    def forward(self, x, w, extra=None):
+        """``extra = (block, x_e)``: one more independent StyleBlock -- a root BasicBlock's shortcut --
+        run as a fifth branch; its output is returned third."""
         x_res, x_tr = x
         # the four StyleBlocks are independent: on a GPU each runs on its own HIP stream (their
         # hundreds of small, launch-bound kernels overlap; a captured graph keeps the branches),
-        # issued in the reference's order so the noise draws keep theirs
-        with ops.Branches(x_res.device, 4) as br:
+        # issued in the reference's order so the noise draws keep theirs (the shortcut's draws
+        # follow the four blocks', as in the reference's BasicBlock)
+        with ops.Branches(x_res.device, 4 + (extra is not None)) as br:
             with br[0]:
                 r_r = self.residual(x_res, w)
             with br[1]:
@@ -369,8 +376,12 @@ class ResnetInit(nn.Module):
                 t_t = self.transient(x_tr, w)
             with br[3]:
                 t_r = self.transient_across(x_tr, w)
-        return (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
-                ops.add_prelu(r_t, t_t, self.activation_transient.weight))
+            if extra is not None:
+                with br[4]:
+                    e = extra[0](extra[1], w)
+        out = (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
+               ops.add_prelu(r_t, t_t, self.activation_transient.weight))
+        return out if extra is None else out + (e,)
 
 
 class SEBlock_conv(nn.Module):
@@ -454,11 +465,15 @@ class BasicBlock(nn.Module):
         else:
             x_a, x_c, x_tr, x_skip, x_tail = ops.route(x, [(0, d), (2 * d, C), (d, C), (0, d), (2 * d, C)])
         x_res = torch.cat([x_a, x_c], 0)
-        r3, t3 = self.rir_3((x_res, x_tr), w)
+        if self.root and SHORTCUT_BRANCH[0]:     # the shortcut StyleBlock beside the four of rir_3
+            r3, t3, sc = self.rir_3((x_res, x_tr), w, extra=(self.shortcut, x_sc))
+        else:
+            r3, t3 = self.rir_3((x_res, x_tr), w)
+            sc = self.shortcut(x_sc, w) if self.root else None
         head_se, head, r_tail = ops.route(r3, [(0, d), (0, d), (d, r3.shape[0])])
         feas_res = ops.scale_add(head, self.se_attention_residual(head_se), x_skip)
         if self.root:
-            sc = prelu(self.shortcut(x_sc, w), self.activation_shortcut.weight)
+            sc = prelu(sc, self.activation_shortcut.weight)
             return torch.cat([feas_res, t3, sc, r_tail], 0)
         return torch.cat([feas_res, t3, x_tail, r_tail], 0)
 
