@@ -919,6 +919,35 @@ def test_conv_wgrad_deterministic(ops, case):
         assert torch.equal(o, outs[0]), float((o - outs[0]).abs().max())
 
 
+@pytest.mark.parametrize("case", WGRAD_DET_CASES)
+def test_conv_fwd_dgrad_deterministic(ops, case):
+    """The same for the forward (LDS-patch conv or gather GEMM with split-K tails) and the input
+    gradient (patch interior + ring fold, or the padded-frame GEMM): eight calls, NaN-poisoned
+    workspaces, equal bits."""
+    B, Cin, H, Cout, k, mode, scaled = case
+    p = (k - 1) // 2
+    geo = ops.conv_geo(B, Cin, H, H, Cout, k, 1, p, mode)
+    g = torch.Generator(device=DEV).manual_seed(sum(case[:6]) + 1)
+    x = torch.randn(Cin, B, H, H, generator=g, device=DEV)
+    gy = torch.randn(Cout, B, H, H, generator=g, device=DEV)
+    w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, generator=g, device=DEV) * 0.1)
+    sx = torch.rand(Cin, B, generator=g, device=DEV) + 0.5 if scaled else None
+    sy = torch.rand(Cout, B, generator=g, device=DEV) + 0.5 if scaled else None
+    for op, fn in ((ops._lib.CONV_FWD, lambda: ops._conv_fwd(geo, x, w, None, sx, sy, 1.0)),
+                   (ops._lib.CONV_DGRAD, lambda: ops._conv_dgrad(geo, gy, w, sy, 1.0))):
+        nb = max(geo.ws_bytes(op, True), geo.ws_bytes(op, False))
+        outs = []
+        with torch.no_grad():
+            for _ in range(8):
+                junk = torch.full((max(nb, 4) // 4 + 1,), float("nan"), device=DEV)
+                del junk
+                outs.append(fn())
+        torch.cuda.synchronize()
+        assert torch.isfinite(outs[0]).all(), op
+        for o in outs[1:]:
+            assert torch.equal(o, outs[0]), (op, float((o - outs[0]).abs().max()))
+
+
 @pytest.mark.parametrize("B,cin,cout,H,k,aligned", [(4, 48, 54, 16, 3, True), (3, 20, 12, 8, 5, True),
                                                     (2, 6, 5, 5, 3, False)])
 def test_modconv_noise_grads(ops, B, cin, cout, H, k, aligned):
