@@ -1,0 +1,14 @@
+#!/bin/bash
+# r05v: the round-5 row-blocked wgrad rewrite (kept under .dev, built as variants): as committed in
+# 61ebbc1, with B staged before A in LDS, with an extra barrier before each K-step's products
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+: > gpurun_out/r05v_race.txt
+for v in v_asis v_bfirst v_bar2; do
+  for s in "8 96 96 64 3 1" "8 96 96 64 5 1" "32 64 64 64 3 0"; do
+    echo "== $v $s" >> gpurun_out/r05v_race.txt
+    GANAMD_SO=tools/variants/$v.so timeout -k 10 120 python3 -u tools/wgrad_race.py $s 30 2>&1 | grep -v amdgpu.ids | tail -n 4 >> gpurun_out/r05v_race.txt || exit $?
+  done
+done
+cat gpurun_out/r05v_race.txt
