@@ -132,6 +132,7 @@ _SIGS = {
     "ganamd_philox_uniform": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_normal": (c_int, [vp, c_long, ctypes.c_uint64, vp, vp]),
     "ganamd_philox_draw": (c_int, [vp, c_long, ctypes.c_uint64, vp, ctypes.c_uint32, c_int, c_int, vp]),
+    "ganamd_philox_draw_keyed": (c_int, [vp, c_long, vp, vp, ctypes.c_uint32, c_int, c_int, vp]),
     "ganamd_philox_advance": (c_int, [vp, vp]),
     "ganamd_critic_create": (vp, [ctypes.POINTER(CriticOp), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "ganamd_critic_destroy": (None, [vp]),
@@ -218,3 +219,26 @@ def capture_id() -> int:
 
 def version() -> str:
     return LIB.ganamd_version().decode()
+
+
+_HIP = []
+
+
+def graph_node_counts(raw_graph: int) -> dict:
+    """Nodes of a captured HIP graph by type (``torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()``):
+    ``kernel`` = the kernel dispatches one replay issues.  Measurement only (bench.py)."""
+    if not _HIP:
+        _HIP.append(ctypes.CDLL("libamdhip64.so"))
+    hip = _HIP[0]
+    g = ctypes.c_void_p(raw_graph)
+    n = ctypes.c_size_t(0)
+    check(hip.hipGraphGetNodes(g, None, ctypes.byref(n)), "hipGraphGetNodes")
+    nodes = (ctypes.c_void_p * max(n.value, 1))()
+    check(hip.hipGraphGetNodes(g, nodes, ctypes.byref(n)), "hipGraphGetNodes")
+    names = {0: "kernel", 1: "memcpy", 2: "memset"}
+    out = {"kernel": 0, "memcpy": 0, "memset": 0, "other": 0}
+    t = ctypes.c_int(0)
+    for i in range(n.value):
+        check(hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)), "hipGraphNodeGetType")
+        out[names.get(t.value, "other")] += 1
+    return out

@@ -15,6 +15,16 @@ moments and step counters are saved too, and so are the device RNG's stream offs
 restored on load even when the resuming process was seeded differently), so a resumed run
 continues the random sequence instead of redrawing the first run's numbers.  Everything is tensors/str/int, so
 ``torch.load(..., weights_only=True)`` reads it.
+
+Data parallel: the replicas' parameters and optimizer state are identical, but every rank draws
+from its OWN Philox key (bench.py seeds rank r with 4321 + r), so rank 0 writes the file with every
+rank's key and offsets (``rng_ranks``, gathered) and each rank resumes its own; a resume at another
+world size keeps each rank's own key and takes rank 0's offsets (distinct keys, distinct streams).
+
+Graph-safe: the load writes every tensor in place (parameters, optimizer moments and step counter,
+BatchNorm statistics, RNG key and offsets), then refreshes the persistent packed conv-weight copies
+(``FlatParams.packs``) that captured graphs launch with -- a graph captured before the load replays
+the loaded state (tests/test_resume_gpu.py).
 """
 from __future__ import annotations
 
@@ -30,6 +40,16 @@ def _is_dist():
 
 def _cpu_state(module):
     return {k: v.detach().to("cpu", copy=True) for k, v in module.state_dict().items()}
+
+
+def _refresh_packed(opt):
+    """Parameters were rewritten in place: refresh the persistent GEMM-order weight copies of the
+    optimizer's flat buffer, which graphs captured before the load launch with (the eager path
+    would repack on the version change; a graph replay does not look)."""
+    flat = getattr(opt, "flat", None)
+    if flat is not None and hasattr(flat, "packs"):
+        flat.epoch += 1
+        flat.packs.repack()
 
 
 def ckpt_path(root, g_name, d_name, method, epoch, i):
@@ -55,8 +75,13 @@ class CheckpointMixin:
                  "optimizer_G": self.optimizer_G.state_dict(), "optimizer_D": self.optimizer_D.state_dict()}
         rng = getattr(self, "rng", None)
         if hasattr(rng, "state"):
-            state["rng"] = {str(k): v.detach().to("cpu") for k, v in rng.state().items()}
-            state["rng_seed"] = int(rng.seed)      # the offsets index THIS key's sequence
+            mine = {"rng": {str(k): v.detach().to("cpu") for k, v in rng.state().items()},
+                    "rng_seed": int(rng.seed)}     # the offsets index THIS key's sequence
+            state.update(mine)
+            if _is_dist():                          # every rank's own key and offsets
+                ranks = [None] * torch.distributed.get_world_size()
+                torch.distributed.all_gather_object(ranks, mine)
+                state["rng_ranks"] = ranks
         path = ckpt_path(self.ckpt_root, self.generator_name, self.discriminator_name, train_name, e, ii)
         err = None
         if not _is_dist() or torch.distributed.get_rank() == 0:
@@ -97,12 +122,20 @@ class CheckpointMixin:
         self.generator.load_state_dict(ck["generator"])
         if "optimizer_G" in ck:
             self.optimizer_G.load_state_dict(ck["optimizer_G"])
+        _refresh_packed(self.optimizer_G)
         self.epoch, self.i = int(ck["epoch"]), int(ck["i"])
         rng = getattr(self, "rng", None)
         if "rng" in ck and hasattr(rng, "set_state"):
-            if "rng_seed" in ck and hasattr(rng, "set_seed") and int(ck["rng_seed"]) != rng.seed:
-                rng.set_seed(int(ck["rng_seed"]))    # a process seeded otherwise resumes the saved key
-            rng.set_state({int(k): v for k, v in ck["rng"].items()})
+            saved, rekey = ck, True
+            if _is_dist():
+                ranks, r = ck.get("rng_ranks"), torch.distributed.get_rank()
+                if ranks is not None and len(ranks) == torch.distributed.get_world_size():
+                    saved = ranks[r]                 # this rank's own key and offsets
+                else:
+                    rekey = False                    # another world size: keep this rank's own key
+            if rekey and "rng_seed" in saved and hasattr(rng, "set_seed") and int(saved["rng_seed"]) != rng.seed:
+                rng.set_seed(int(saved["rng_seed"]))  # a process seeded otherwise resumes the saved key
+            rng.set_state({int(k): v for k, v in saved["rng"].items()})
         return True
 
     def load_discriminator_ckpt(self, name):
@@ -113,4 +146,5 @@ class CheckpointMixin:
         self.discriminator.load_state_dict(ck["discriminator"])
         if "optimizer_D" in ck:
             self.optimizer_D.load_state_dict(ck["optimizer_D"])
+        _refresh_packed(self.optimizer_D)
         return True

@@ -31,8 +31,10 @@
 #include <stdint.h>
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "../../include/ganamd.h"
@@ -2231,10 +2233,71 @@ bool desc_ok(const ganamd_conv_desc* d) {
          extents_ok(d);
 }
 
+// The workspace query's answer per (device, descriptor, op), so the size check of every conv call
+// does not re-plan (the query runs two or three planner evaluations): an open-addressed table of
+// whole-descriptor keys under a lock (calls may come from several threads); a full table is cleared.
+struct WsKey {
+  ganamd_conv_desc d;
+  int op, dev;
+};
+struct WsSlot {
+  WsKey k;
+  size_t need;
+  bool used;
+};
+constexpr int kWsSlots = 4096;
+WsSlot g_ws_cache[kWsSlots];
+int g_ws_count = 0;
+std::mutex g_ws_mu;
+
+uint64_t ws_hash(const WsKey& k) {
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(&k);
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < sizeof(WsKey); ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return h;
+}
+
 // the call's workspace against the query for its descriptor (GANAMD_EINVAL when short or missing)
 int ws_check(const ganamd_conv_desc* d, int op, const void* workspace, size_t workspace_bytes) {
+  WsKey k;
+  memset(&k, 0, sizeof(k));
+  k.d = *d;
+  k.op = op;
+  if (hipGetDevice(&k.dev) != hipSuccess) k.dev = -1;
+  const uint64_t h = ws_hash(k);
   size_t need = 0;
-  if (ganamd_conv_workspace(d, op, &need) != GANAMD_OK) return GANAMD_EINVAL;
+  bool hit = false;
+  {
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    for (int i = 0; i < kWsSlots; ++i) {
+      WsSlot& sl = g_ws_cache[(h + i) % kWsSlots];
+      if (!sl.used) break;
+      if (memcmp(&sl.k, &k, sizeof(k)) == 0) {
+        need = sl.need;
+        hit = true;
+        break;
+      }
+    }
+  }
+  if (!hit) {
+    if (ganamd_conv_workspace(d, op, &need) != GANAMD_OK) return GANAMD_EINVAL;
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    if (2 * (g_ws_count + 1) > kWsSlots) {        // keep probes short: start over when half full
+      for (auto& sl : g_ws_cache) sl.used = false;
+      g_ws_count = 0;
+    }
+    for (int i = 0; i < kWsSlots; ++i) {
+      WsSlot& sl = g_ws_cache[(h + i) % kWsSlots];
+      if (!sl.used) {
+        sl.k = k;
+        sl.need = need;
+        sl.used = true;
+        ++g_ws_count;
+        break;
+      }
+      if (memcmp(&sl.k, &k, sizeof(k)) == 0) break;
+    }
+  }
   return need && (!workspace || workspace_bytes < need) ? GANAMD_EINVAL : GANAMD_OK;
 }
 

@@ -6,7 +6,9 @@
 //   normal   Box-Muller on word pairs: r = sqrt(-2 ln u1), u1 = ((w0 >> 8) + 1) * 2^-24 in (0, 1],
 //            z0 = r cos(2 pi u2), z1 = r sin(2 pi u2), u2 = (w1 >> 8) * 2^-24
 // The stream offset lives in device memory and is advanced by one per call (a one-thread launch
-// after the draw), so a captured graph draws fresh numbers on every replay.
+// after the draw), so a captured graph draws fresh numbers on every replay.  The key may live in
+// device memory too (ganamd_philox_draw_keyed): a graph captured before a re-key (a checkpoint
+// resume) then draws with the new key on its next replay.
 //
 // Concurrent consumers never share a counter:
 //   * each consumer owns its offset word (rng.py DeviceRNG.fork gives stream s the offsets
@@ -48,8 +50,10 @@ __device__ __forceinline__ void philox10(uint32_t (&c)[4], uint64_t seed) {
 
 template <bool NORMAL>
 __global__ __launch_bounds__(kNT) void philox_kernel(float* __restrict__ out, long n, uint64_t seed,
+                                                     const uint64_t* __restrict__ key,
                                                      const uint64_t* __restrict__ offset, uint32_t sub) {
   const uint64_t off = *offset;
+  if (key) seed = *key;
   const long groups = (n + 3) / 4;
   const bool aligned = ((uintptr_t)out & 15) == 0;
   for (long g = blockIdx.x * (long)kNT + threadIdx.x; g < groups; g += (long)gridDim.x * kNT) {
@@ -85,16 +89,16 @@ __global__ __launch_bounds__(kNT) void philox_kernel(float* __restrict__ out, lo
 
 __global__ void offset_advance_kernel(uint64_t* offset) { *offset += 1; }
 
-int launch(bool normal, float* out, long n, uint64_t seed, uint64_t* offset, uint32_t sub, bool advance,
-           hipStream_t st) {
+int launch(bool normal, float* out, long n, uint64_t seed, const uint64_t* key, uint64_t* offset, uint32_t sub,
+           bool advance, hipStream_t st) {
   if (!out || !offset || n <= 0) return GANAMD_EINVAL;
   const long groups = (n + 3) / 4;
   if (sub != 0 && groups > (1L << 32)) return GANAMD_EINVAL;    // word 1 must hold the index alone
   const unsigned blocks = (unsigned)std::min<long>((groups + kNT - 1) / kNT, 2048L * 8);
   if (normal)
-    hipLaunchKernelGGL(philox_kernel<true>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, offset, sub);
+    hipLaunchKernelGGL(philox_kernel<true>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, key, offset, sub);
   else
-    hipLaunchKernelGGL(philox_kernel<false>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, offset, sub);
+    hipLaunchKernelGGL(philox_kernel<false>, dim3(blocks), dim3(kNT), 0, st, out, n, seed, key, offset, sub);
   if (advance) hipLaunchKernelGGL(offset_advance_kernel, dim3(1), dim3(1), 0, st, offset);
   return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
 }
@@ -104,16 +108,22 @@ int launch(bool normal, float* out, long n, uint64_t seed, uint64_t* offset, uin
 extern "C" {
 
 int ganamd_philox_uniform(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream) {
-  return launch(false, out, n, seed, offset, 0, true, stream);
+  return launch(false, out, n, seed, nullptr, offset, 0, true, stream);
 }
 
 int ganamd_philox_normal(float* out, long n, uint64_t seed, uint64_t* offset, hipStream_t stream) {
-  return launch(true, out, n, seed, offset, 0, true, stream);
+  return launch(true, out, n, seed, nullptr, offset, 0, true, stream);
 }
 
 int ganamd_philox_draw(float* out, long n, uint64_t seed, uint64_t* offset, uint32_t sub, int normal, int advance,
                        hipStream_t stream) {
-  return launch(normal != 0, out, n, seed, offset, sub, advance != 0, stream);
+  return launch(normal != 0, out, n, seed, nullptr, offset, sub, advance != 0, stream);
+}
+
+int ganamd_philox_draw_keyed(float* out, long n, const uint64_t* key, uint64_t* offset, uint32_t sub, int normal,
+                             int advance, hipStream_t stream) {
+  if (!key) return GANAMD_EINVAL;
+  return launch(normal != 0, out, n, 0, key, offset, sub, advance != 0, stream);
 }
 
 int ganamd_philox_advance(uint64_t* offset, hipStream_t stream) {

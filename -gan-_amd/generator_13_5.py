@@ -368,6 +368,7 @@ class ResnetInit(nn.Module):
         # issued in the reference's order so the noise draws keep theirs (the shortcut's draws
         # follow the four blocks', as in the reference's BasicBlock)
         with ops.Branches(x_res.device, 4 + (extra is not None)) as br:
+            br.share(x_res, x_tr, None if extra is None else extra[1])
             with br[0]:
                 r_r = self.residual(x_res, w)
             with br[1]:
@@ -648,7 +649,9 @@ class _NoiseHub:
         shapes = self.shapes.get(batch)
         if bulk is not None and shapes:
             total = sum(C * B * H * W for B, C, H, W in shapes)
-            self._bulk = (bulk(total), list(shapes), 0, 0)
+            buf = bulk(total)
+            ops.branch_share(buf)       # its views are saved by ops on the branch streams
+            self._bulk = (buf, list(shapes), 0, 0)
 
     def end(self, batch):
         if self._rec is not None:

@@ -1415,7 +1415,10 @@ class Branches:
     build had, makes sibling branches fork and join through the same inner streams, serialising
     them and letting the allocator recycle one sibling's inner blocks while the other still reads
     them; the k3/k5 split inside the parallel StyleBlocks also measured slower, 37.9 vs 39.8
-    img/s.)  On the CPU, or with BRANCH_STREAMS[0] False, the bodies run inline."""
+    img/s.)  On the CPU, or with BRANCH_STREAMS[0] False, the bodies run inline.
+
+    Current-stream tensors the branches read must be passed to ``share`` (or ``branch_share``):
+    the branches' backward nodes release them from their own streams."""
 
     _depth = [0]
 
@@ -1447,3 +1450,35 @@ class Branches:
 
     def __getitem__(self, i):
         return torch.cuda.stream(self.streams[i]) if self.on else contextlib.nullcontext()
+
+    def share(self, *tensors):
+        """Tensors made on the current stream that the branches read: see ``branch_share``."""
+        if self.on:
+            _record(tensors, self.streams)
+
+
+def _record(tensors, streams):
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            for s in streams:
+                t.record_stream(s)
+
+
+def branch_share(*tensors):
+    """Mark current-stream tensors that branch-stream work reads -- in the forward, or in the
+    backward through a branch op's saved tensors -- as used by every pooled branch stream.
+
+    The backward of a branch op runs on that branch's stream (autograd keeps the forward's stream)
+    and releases its saved tensors when it has been ISSUED, not when its kernels have run: without
+    this, a block allocated on the main stream (a branch's input, a view of the forward's bulk noise
+    draw) could be handed by the caching allocator to a main-stream kernel while a branch kernel still
+    reads it -- a race whose outcome depends on timing (under graph capture: a missing edge in the
+    graph).  With the streams recorded, the allocator reuses such a block only after the branch
+    streams' work queued at the free has finished (during a capture: after the capture)."""
+    if not BRANCH_STREAMS[0]:
+        return
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            pool = _STREAM_POOL.get(t.device.index if t.device.index is not None else torch.cuda.current_device())
+            if pool:
+                _record((t,), pool)

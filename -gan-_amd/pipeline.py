@@ -64,6 +64,8 @@ class Iteration:
         self.allreduce = allreduce if allreduce is not None else (allreduce_mean_ if world > 1 else _sync_none)
         self.graphs = {}
         self._captured = False
+        self.count_nodes = False        # set before capture(): count each graph's nodes (dispatches)
+        self.nodes = {}
 
     def _fakes(self, k):
         tr = self.tr
@@ -102,9 +104,13 @@ class Iteration:
         # left its eager peak behind)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=self.count_nodes)
         with torch.cuda.graph(g, pool=pool):
             fn()
+        if self.count_nodes:            # dispatches per replay (bench.py reports them per iteration)
+            from ._lib import graph_node_counts
+            self.nodes[id(g)] = graph_node_counts(g.raw_cuda_graph())
+            g.instantiate()
         if os.environ.get("DP_MEMLOG") == "1":
             torch.cuda.synchronize()
             print(f"[mem] captured {getattr(fn, '__name__', fn)}: allocated {torch.cuda.memory_allocated() / 2**30:.1f} "
@@ -192,6 +198,20 @@ class Iteration:
         if "gstep" in g:
             self.allreduce(self.tr.optimizer_G.flat.grad)
             g["gstep"].replay()
+
+    def dispatches(self):
+        """Graph nodes one ``step()`` replays, by type (``count_nodes`` set before ``capture``):
+        the fake groups once each, the critic (and AdamW) graphs n_critic times, the generator
+        step once."""
+        g = self.graphs
+        reps = [(x, 1) for x in g.get("fake", [])] + [(g["critic"], self.n_critic)]
+        reps += [(g["dstep"], self.n_critic)] if "dstep" in g else []
+        reps += [(g["gen"], 1)] + ([(g["gstep"], 1)] if "gstep" in g else [])
+        out = {}
+        for x, k in reps:
+            for key, v in self.nodes.get(id(x), {}).items():
+                out[key] = out.get(key, 0) + k * v
+        return out
 
     def phase_ms(self):
         """One replay per phase graph, each timed alone (outside the timed region; N = 1).  The

@@ -12,6 +12,12 @@ import torch
 from . import _lib
 
 
+def _signed64(v: int) -> int:
+    """A uint64 key as the int64 with the same bits (the key tensor's dtype)."""
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
 class DeviceRNG:
     """Philox4x32-10 draws on the device (csrc/rng.hip, ganamd_philox_*).
 
@@ -33,13 +39,17 @@ class DeviceRNG:
 
     STREAM_SHIFT = 40
 
-    def __init__(self, device, seed: int | None = None, stream: int = 0):
+    def __init__(self, device, seed: int | None = None, stream: int = 0, _key=None):
         self.device = torch.device(device)
         if seed is None:
             seed = torch.cuda.initial_seed() if self.device.type == "cuda" else torch.initial_seed()
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.stream = int(stream)
         self.offset = torch.full((1,), self.stream << self.STREAM_SHIFT, dtype=torch.int64, device=self.device)
+        # the Philox key in device memory (ganamd_philox_draw_keyed), shared with every fork: a
+        # re-key is one in-place write that graphs captured before it see on their next replay
+        self.key = _key if _key is not None else torch.full((1,), _signed64(self.seed), dtype=torch.int64,
+                                                            device=self.device)
         self.log = None              # list: record (stream, offset, sub, n) of eager draws (tests)
         self._forks = {}
 
@@ -47,7 +57,7 @@ class DeviceRNG:
         """Stream ``stream`` of this seed (one per (parent, stream): the same object every call)."""
         r = self._forks.get(stream)
         if r is None:
-            r = self._forks[stream] = DeviceRNG(self.device, self.seed, self.stream + stream)
+            r = self._forks[stream] = DeviceRNG(self.device, self.seed, self.stream + stream, _key=self.key)
         return r
 
     def _draw(self, normal, shape, sub=0, advance=True):
@@ -56,8 +66,8 @@ class DeviceRNG:
         if n:
             if self.log is not None:
                 self.log.append((self.stream, int(self.offset.item()), sub, n))
-            _lib.check(_lib.LIB.ganamd_philox_draw(out.data_ptr(), n, self.seed, self.offset.data_ptr(), sub,
-                                                   int(normal), int(advance), _lib.stream()), "philox_draw")
+            _lib.check(_lib.LIB.ganamd_philox_draw_keyed(out.data_ptr(), n, self.key.data_ptr(), self.offset.data_ptr(),
+                                                         sub, int(normal), int(advance), _lib.stream()), "philox_draw")
         return out
 
     def randn(self, shape):
@@ -87,9 +97,11 @@ class DeviceRNG:
         return {s: r.offset.clone() for s, r in [(self.stream, self)] + [(f.stream, f) for f in self._forks.values()]}
 
     def set_seed(self, seed: int):
-        """Re-key this generator and its forks (a resumed run continues the SAVED seed's sequence;
-        graphs captured before this keep the key they were captured with)."""
+        """Re-key this generator and its forks (a resumed run continues the SAVED seed's sequence).
+        The key is written in place on the device, so graphs captured before this draw with the new
+        key from their next replay on, as the eager path does."""
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.key.fill_(_signed64(self.seed))
         for f in self._forks.values():
             f.set_seed(self.seed)
 

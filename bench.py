@@ -486,6 +486,7 @@ def main():
     step = iteration
     graphs = {}
     if args.mode == "graph" and pipelined:
+        it.count_nodes = True          # the iteration's dispatch count (graph nodes per replay)
         it.capture()
         step = it.step
         if rank == 0:
@@ -607,6 +608,9 @@ def main():
             if pipelined:
                 out["config"]["fake_groups"] = it.groups
                 out["config"]["fake_overlap"] = it.overlap
+                if it.nodes:
+                    # kernel dispatches (graph kernel nodes) of one replayed iteration, and the rest
+                    out["dispatches_per_iter"] = it.dispatches()
             achieved = ALGO_GFLOP_PER_IMAGE * 1e9 * B / t_iter / 1e12      # per GPU
             out["roofline"] = dict(probe or {}, **{
                 # whole iteration: algorithmic FLOPs / iteration time, per GPU

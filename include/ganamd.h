@@ -439,6 +439,11 @@ int ganamd_philox_normal(float* out, long n, uint64_t seed, uint64_t* offset, hi
  * s * 2^40), so no two draws of an iteration share a counter. */
 int ganamd_philox_draw(float* out, long n, uint64_t seed, uint64_t* offset, uint32_t sub, int normal, int advance,
                        hipStream_t stream);
+/* The same draw with the key read on the device from *key (one uint64, non-NULL): re-keying the
+ * generator (a checkpoint resume, rng.py DeviceRNG.set_seed) is then a device write that graphs
+ * captured before it see on their next replay, as they see the offset. */
+int ganamd_philox_draw_keyed(float* out, long n, const uint64_t* key, uint64_t* offset, uint32_t sub, int normal,
+                             int advance, hipStream_t stream);
 int ganamd_philox_advance(uint64_t* offset, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------

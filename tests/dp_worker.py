@@ -12,7 +12,8 @@ critic's parameters after its step to the path given as argv[1].
 progan schedule (pipeline.Iteration, fake batches one per critic step on a side stream) at
 B = 64 per rank, one iteration; rank 0 writes both models' parameters and gradients.
 
-``dp_worker.py OUT graph SCHEDULE [B]``: the bench's N > 1 graph-mode path instead -- one pipelined
+``dp_worker.py OUT graph SCHEDULE [B]`` (2 ranks; 8 ranks for config 3's world size): the bench's
+N > 1 graph-mode path instead -- one pipelined
 WGAN-GP iteration (gan_amd.pipeline.Iteration: captured fake-batch / critic / AdamW / generator
 graphs, the next fake batch on a side stream, the flat-gradient all-reduce eagerly between graphs)
 at B per rank (default 8; 64 = config 3's per-GPU batch) with device Philox streams seeded per rank;
@@ -129,11 +130,13 @@ def main_graph(out):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     _mem("eager warm-up")
-    # the ranks capture one after another: both share one GPU here, and a capture peaks at the
-    # graph pools plus one phase's eager warm-up (~140 GB per rank at B = 64)
+    # the ranks capture one after another: they share one GPU here, and a capture peaks at the
+    # graph pools plus one phase's eager warm-up (~140 GB per rank at B = 64; with eight ranks the
+    # captures of the others' would add up)
     for r in range(world):
         if r == rank:
             it.capture()
+            print(f"[rank {rank}] captured", flush=True)
         dist.barrier()
     _mem("captured")
     restore(tr, snap)

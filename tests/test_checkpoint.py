@@ -98,3 +98,57 @@ def test_checkpoint_restores_rng_seed(tmp_path):
     assert tr2.load_generator_ckpt(name)
     assert tr2.rng.seed == 1234 and data.seed == 1234 and int(tr2.rng.offset) == 5
 
+
+
+def _dp_ckpt_worker(rank, world, port, root, out):
+    """One rank of the DP checkpoint test: every rank draws with its own key (bench.py: 4321 + rank),
+    saves (rank 0 writes), then a fresh trainer seeded otherwise resumes."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _pp, tr = _trainer(root)
+    tr.rng = gan_amd.DeviceRNG("cpu", seed=4321 + rank)
+    with torch.no_grad():
+        tr.rng.offset.fill_(10 + rank)
+        tr.rng.fork(2).offset.fill_((2 << tr.rng.STREAM_SHIFT) + 20 + rank)
+    name = os.path.splitext(os.path.basename(tr.save_ckpt("WGANGP", 0, 0)))[0]
+    _pp2, tr2 = _trainer(root)
+    tr2.rng = gan_amd.DeviceRNG("cpu", seed=7)
+    data = tr2.rng.fork(2)
+    assert tr2.load_generator_ckpt(name)
+    res = torch.tensor([tr2.rng.seed, int(tr2.rng.key), int(tr2.rng.offset), int(data.offset), data.seed],
+                       dtype=torch.float64)
+    got = [torch.zeros_like(res) for _ in range(world)]
+    dist.all_gather(got, res)
+    if rank == 0:
+        torch.save(torch.stack(got), out)
+    dist.destroy_process_group()
+
+
+def test_dp_checkpoint_keeps_each_ranks_stream(tmp_path):
+    """rank 0 writes the file, but every rank resumes ITS OWN Philox key and
+    offsets, so the ranks keep drawing different z / noise / eps / data after a DP resume."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "ranks.pt")
+    mp.spawn(_dp_ckpt_worker, args=(2, port, tmp_path, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    for r in range(2):
+        seed, key, off, doff, dseed = (int(v) for v in got[r])
+        assert seed == key == dseed == 4321 + r, (r, got)
+        assert off == 10 + r and doff == (2 << 40) + 20 + r, (r, got)
+
+
+def test_rekey_reaches_forks_in_place():
+    """set_seed writes the device key in place (graphs captured before it see it) and forks share it."""
+    rng = gan_amd.DeviceRNG("cpu", seed=(1 << 64) - 3)
+    data = rng.fork(2)
+    ptr = rng.key.data_ptr()
+    assert int(rng.key) == -3 and data.key.data_ptr() == ptr
+    rng.set_seed(99)
+    assert rng.key.data_ptr() == ptr and int(data.key) == 99 and data.seed == 99

@@ -232,6 +232,54 @@ def _dp_errors(got, tr, g0, d0):
     return errs
 
 
+def test_dp_graph_eight_ranks_match_shard_mean(tmp_path):
+    """Config 3's world size: EIGHT ranks (gloo, all on this GPU) run the bench's
+    N > 1 graph schedule for G13_5 / D9_4 -- pipeline.Iteration with fake groups (4, 1), the fifth
+    fake batch on the side stream during critic steps 1-4, their all-reduces and AdamW -- at B = 8
+    per rank, per-rank Philox seeds.  The first all-reduced critic gradient must equal the shard
+    mean at 1e-6; after the whole iteration the bar is 3x the shard mean's own spread under the
+    opposite summation order (gloo's ring adds eight buffers in another order than the hand-made
+    mean, and the iteration amplifies last-bit differences -- the 4-rank progan test's bar)."""
+    W, B = 8, 8
+    out = str(tmp_path / "rank0_graph8.pt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={W}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
+           "graph", "overlap", str(B)]
+    env = _env()
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run(cmd, cwd=REPO, env=env, timeout=1500, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert got["world"] == W and got["batch"] == B and got["d_grad0"] is not None
+    print(f"rank 0: peak {got['peak_reserved'] / 2**30:.1f} GiB reserved")
+
+    import gan_amd
+    dev = torch.device("cuda", 0)
+
+    def shard_mean(reverse):
+        G, D = dp_worker.make_models(gan_amd, dev)
+        tr = gan_amd.Train([], dev, 1, 256, G, "G13_5", D, "D9_4", rng=gan_amd.DeviceRNG(dev, 1))
+        g0, d0 = tr.optimizer_G.flat.data.detach().cpu().clone(), tr.optimizer_D.flat.data.detach().cpu().clone()
+        rngs = [gan_amd.DeviceRNG(dev, dp_worker.graph_seed(q)) for q in range(W)]
+        first = _shard_mean_iteration(tr, rngs, B, list(dp_worker.GRAPH_FAKE_GROUPS), reverse=reverse)
+        return tr, g0, d0, first
+
+    tr, g0, d0, first = shard_mean(False)
+    errs = _dp_errors(got, tr, g0, d0)
+    errs["d_grad0"] = _rel(got["d_grad0"], first)
+    mid = {k: v.detach().cpu().clone() for k, v in (("g_data", tr.optimizer_G.flat.data),
+                                                   ("g_grad", tr.optimizer_G.flat.grad),
+                                                   ("d_data", tr.optimizer_D.flat.data),
+                                                   ("d_grad", tr.optimizer_D.flat.grad))}
+    del tr
+    tr2, _, _, _ = shard_mean(True)
+    spread = _dp_errors(mid, tr2, g0, d0)
+    print(f"G13_5 {W}-rank graph DP vs shard mean: {errs}; shard-mean spread under reverse order: {spread}")
+    assert errs["d_grad0"] < 1e-6, errs
+    for k in ("g_grad", "d_grad", "g_data", "d_data", "g_move", "d_move"):
+        assert errs[k] <= max(3 * spread[k], 1e-5), (k, errs, spread)
+
+
 def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
     out = str(tmp_path / "rank0_progan.pt")
     W = dp_worker.PROGAN_WORLD
@@ -284,12 +332,18 @@ def test_dp_progan_four_ranks_match_shard_mean(tmp_path):
         assert errs[k] <= max(3 * spread[k], 1e-5), (k, errs, spread)
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph"])
-def test_bench_two_ranks(mode):
-    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--batch", "8",
+@pytest.mark.parametrize("mode,n", [("eager", 2), ("graph", 2), ("graph", 8)])
+def test_bench_ranks(mode, n):
+    """``bench.py --gpus N --backend gloo`` starts its own N ranks (the driver's N = 8 launch path:
+    launch_ranks, per-rank seeds, the N > 1 side-stream schedule) and reports n_gpus N."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--backend", "gloo", "--batch", "8",
            "--steps", "1", "--warmup", "1", "--mode", mode, "--no-cpu-baseline", "--no-extras"]
-    r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
+    env = _env()
+    if n > 2:
+        env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run(cmd, cwd=REPO, env=env, timeout=1500, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
-    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 16 and res["value"] > 0, res
+    assert res["n_gpus"] == n and res["config"]["global_batch"] == 8 * n and res["value"] > 0, res
+    assert res["config"]["parallelism"] == f"dp{n}" and res["config"]["fake_overlap"] is True, res

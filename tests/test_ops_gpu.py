@@ -802,6 +802,11 @@ SPLIT6_CASES = [
     ("fwd", 32, 96, 64, 96, 5, 1, 2, True, "split6 LDS-patch conv, 96 rows (32x32x16)"),
     ("fwd", 32, 48, 64, 48, 5, 1, 2, True, "split6 LDS-patch conv, 48 rows (paired 16x16x32)"),
     ("dgrad", 32, 96, 64, 96, 5, 1, 2, True, "split6 LDS-patch dgrad interior + ring GEMM"),
+    # the 64-row patch tile (Cout in (48, 64]) at W = 64 and W = 32, forward and dgrad
+    ("fwd", 32, 56, 64, 56, 3, 1, 1, False, "split6 LDS-patch conv, 64-row tile, W=64"),
+    ("dgrad", 32, 56, 64, 56, 3, 1, 1, False, "split6 LDS-patch dgrad, 64-row tile, W=64"),
+    ("fwd", 32, 64, 32, 60, 3, 1, 1, True, "64-row tile at W=32 (scaled, Cout 60)"),
+    ("dgrad", 32, 60, 32, 64, 3, 1, 1, True, "64-row dgrad at W=32 (scaled, Cin 60)"),
 ]
 
 
@@ -811,10 +816,27 @@ def test_split6_fp32_class(ops, case):
     full-mantissa random operands -- or, on launches of millions of outputs whose error tail fp32
     accumulation alone takes past 1e-6, within 2x of the same convolution evaluated in float32 on
     the host: the split products are fp32-class."""
+    _split6_check(ops, case, 600 + SPLIT6_CASES.index(case))
+
+
+def test_split6_wide_gather_tile(ops):
+    """the 128x256 gather tile the planner picks by cost (unscaled 128->128 3x3 at
+    32x32) against float64 -- at the first batch whose plan on this GPU is that tile."""
+    for B in (128, 256, 160, 192, 64, 96):
+        g = ops.conv_geo(B, 128, 32, 32, 128, 3, 1, 1)
+        info = ops.plan_info(g, 0, False)
+        if info["kernel"] == 0 and info["bn"] == 256:
+            break
+    else:
+        pytest.fail("no batch plans the 128x256 tile")
+    _split6_check(ops, ("fwd", B, 128, 32, 128, 3, 1, 1, False, "128x256 gather tile (costed)"), 650, want_bn=256)
+
+
+def _split6_check(ops, case, seed, want_bn=None):
     from tests._emu import emulate, max_rel
     op, B, cin, H, cout, k, s, p, scaled, _kind = case
     g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
-    gen = torch.Generator().manual_seed(600 + SPLIT6_CASES.index(case))
+    gen = torch.Generator().manual_seed(seed)
     x = torch.randn(cin, B, H, H, generator=gen).to(DEV)
     w = torch.nn.Parameter(torch.randn(cout, cin, k, k, generator=gen).to(DEV))
     gy = torch.randn(cout, B, g.OH, g.OW, generator=gen).to(DEV)
@@ -835,6 +857,10 @@ def test_split6_fp32_class(ops, case):
     info = ops.plan_info(g, {"fwd": 0, "dgrad": 1}[op], scaled) if op != "wgrad" else {}
     if "patch" in case[-1]:
         assert info["kernel"] == 1, info
+    if "64-row" in case[-1] and info.get("kernel") == 1:
+        assert info["bm"] == 64, info
+    if want_bn is not None:
+        assert info["bn"] == want_bn, info
     print(f"{case[-1]}: max rel err vs float64 {e:.2e} (vs a bf16-operand GEMM {e_bf:.2e}); plan {info}")
     if e > 1e-6:
         # millions of outputs: compare with fp32's own error tail -- a host float32 evaluation and
