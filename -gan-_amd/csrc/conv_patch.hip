@@ -53,7 +53,7 @@ constexpr int kMaxScale = 1024;   // input channels whose scales the block stage
 #define GANAMD_P96_NW 12          // waves of a 96-row block at W = 64
 #endif
 #ifndef GANAMD_P96_MB
-#define GANAMD_P96_MB 32          // MFMA block edge of the 96-row blocks (16: paired 16x16x32)
+#define GANAMD_P96_MB 16          // MFMA block edge of the 96-row 5x5 blocks at W = 64 (16: paired 16x16x32)
 #endif
 #ifndef GANAMD_P48_NW
 #define GANAMD_P48_NW 8           // waves of a 48-row block at W = 64
@@ -61,8 +61,8 @@ constexpr int kMaxScale = 1024;   // input channels whose scales the block stage
 #ifndef GANAMD_P_UNROLL4
 #define GANAMD_P_UNROLL4 1        // fully unroll the tap loop of the 4-wave 5x5 blocks (3x3: a loop of tap pairs)
 #endif
-#ifndef GANAMD_P16_DEDUP
-#define GANAMD_P16_DEDUP 0        // 16x16 paths: two B fragment reads per 16 channels instead of three
+#ifndef GANAMD_P16_ADUP
+#define GANAMD_P16_ADUP 0         // 16x16 paths: pair-low lanes load h for X2 too (no select; +1/3 weight bytes)
 #endif
 #ifndef GANAMD_P64
 #define GANAMD_P64 1              // a 64-row tile for 48 < M <= 64 (else the 96-row one, a third empty)
@@ -123,11 +123,15 @@ __device__ __forceinline__ int mfma_row(int lane, int r) {
 template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
 __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int NT = 64 * NW;
-  constexpr int MB = (BM % 32 == 0) ? (BM == 96 ? GANAMD_P96_MB : 32) : 16;   // MFMA block edge (48 rows: 16)
+  constexpr int MB = (BM % 32 == 0) ? ((BM == 96 && TW == 64 && KK == 5) ? GANAMD_P96_MB : 32) : 16;   // MFMA block edge (48 rows: 16)
   // waves along M: blocks of 4 waves per 32 rows (the 12-wave 96-row and 8-wave 64-row blocks) give
   // each wave 32 rows x 128 pixels (a third / half of the weight fragments per wave, 3 / 2 waves per
-  // SIMD); otherwise every wave owns all rows
-  constexpr int WM = (MB == 32 && NW % 4 == 0 && BM % (32 * (NW / 4)) == 0) ? NW / 4 : 1, WN = NW / WM;
+  // SIMD); the 8-wave 96-row block on 16x16 fragments gives each wave 48 rows x 128 pixels (2 waves
+  // per SIMD); otherwise every wave owns all rows
+  constexpr int WM = (MB == 32 && NW % 4 == 0 && BM % (32 * (NW / 4)) == 0) ? NW / 4
+                     : (MB == 16 && BM == 96 && NW == 8) ? 2 : 1,
+                WN = NW / WM;
+  constexpr int NA = MB == 32 ? 3 : 2;                      // A fragment registers per row block
   constexpr int PW = NPIX / WN;                             // pixels per wave
   constexpr int TM = BM / (MB * WM), TN = PW / MB, NR = MB == 32 ? 16 : 4;
   using acc_t = typename std::conditional<MB == 32, f32x16, f32x4>::type;
@@ -209,23 +213,33 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   };
 
   // ---- A fragments of one tap from global memory (pre-split planes).  32x32: lane (r, h) holds
-  // rows m0 + 32i + r, k = 8h .. 8h+7 of the three planes.  16x16 paired: lane (r, q), k-half
-  // hf = q & 1, pair hi = q >> 1: (h|m), (h|l), (m|h) (see mfma below).
+  // rows m0 + 32i + r, k = 8h .. 8h+7 of the three planes.  16x16 paired (lane (r, q): k-half
+  // hf = q & 1 of the 16 channels, pair half hi = q >> 1): two fragments, X1 = (h|m) and X2 = (h|l)
+  // -- lanes with hi = 0 hold h in both, so they load it once (load 0) and their second load is an
+  // out-of-range offset (no memory traffic, hardware zero) that the product step replaces by load 0:
+  // 1.5 planes of weight bytes per 16 rows, the 32x32 form's 3 planes per 32 rows.
   const int fr = MB == 32 ? (lane & 31) : (lane & 15);
   const int fhalf = MB == 32 ? (lane >> 5) : ((lane >> 4) & 1);
   const int fhi = MB == 32 ? 0 : (lane >> 5);
   int a_row[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) a_row[i] = 2 * (((m0 + wrow + i * MB + fr) * nct * T) * 16 + 8 * fhalf);   // bytes
-  const int pl0 = MB == 32 ? 0 : (fhi ? 1 : 0), pl1 = MB == 32 ? 1 : (fhi ? 2 : 0), pl2 = MB == 32 ? 2 : (fhi ? 0 : 1);
   const int wpb = 2 * p.wplane;                             // plane stride in bytes
-  auto a_load = [&](int kt, bf16x8 (&fa)[TM][3]) {
+  auto a_load = [&](int kt, bf16x8 (&fa)[TM][NA]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int o = a_row[i] + kt * 32;
-      fa[i][0] = bload8h(rw, o + pl0 * wpb);
-      fa[i][1] = bload8h(rw, o + pl1 * wpb);
-      fa[i][2] = bload8h(rw, o + pl2 * wpb);
+      if constexpr (MB == 32) {
+        fa[i][0] = bload8h(rw, o);
+        fa[i][1] = bload8h(rw, o + wpb);
+        fa[i][2] = bload8h(rw, o + 2 * wpb);
+      } else {
+        fa[i][0] = bload8h(rw, o + (fhi ? wpb : 0));              // h | m
+        if constexpr (GANAMD_P16_ADUP)
+          fa[i][1] = bload8h(rw, o + (fhi ? 2 * wpb : 0));        // h | l
+        else
+          fa[i][1] = bload8h(rw, fhi ? o + 2 * wpb : kOOB);       // - | l
+      }
     }
   };
 
@@ -236,22 +250,28 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
     const int q = wcol + j * MB + fr;
     posb[j] = (q / TW) * PWD + q % TW;
   }
-  const int bq0 = 0, bq1 = MB == 32 ? 1 : (fhi ? 0 : 1), bq2 = MB == 32 ? 2 : (fhi ? 2 : 1);
-  // the three B fragments of column block j at tap offset toff
+  // the three B fragments of column block j at tap offset toff: the planes h, m, l (32x32); for the
+  // paired 16x16 products Y1 = (h|h), Y2 = (m|m), Y3 = (l|h) -- the third read takes its plane from
+  // a per-lane offset (pair-high lanes read h again), so the product step needs no select: one
+  // v_cndmask per dword per column block per tap would cost more issue slots than the 16x16x32
+  // MFMAs leave free (8 of their 16 cycles)
+  // (16x16: the plain layout is linear in the position, so each column block's lane address is a
+  // per-lane byte base plus the tap's uniform offset -- one address add per read group)
+  const int pl3 = MB == 32 ? 2 * PS : (fhi ? 0 : 2 * PS);
+  int pbyte[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) pbyte[j] = 2 * poff<MB>(posb[j], fhalf);
   auto b_frag = [&](const unsigned short* P, int toff, int j, bf16x8 (&f)[3]) {
-    const int o = poff<MB>(posb[j] + toff, fhalf);
-    if constexpr (MB == 16 && GANAMD_P16_DEDUP) {
-      // paired 16x16x32: a lane's three B fragments hold only two distinct planes -- h and
-      // X = (pair hi ? l : m) -- (h|h), (m|h), (m|l): read each once, the middle one is a select
-      const bf16x8 h = *reinterpret_cast<const bf16x8*>(&P[o]);
-      const bf16x8 x = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
-      f[0] = h;
-      f[1] = fhi ? h : x;
-      f[2] = x;
+    if constexpr (MB == 16) {
+      const char* q = reinterpret_cast<const char*>(P) + toff * 32 + pbyte[j];
+      f[0] = *reinterpret_cast<const bf16x8*>(q);
+      f[1] = *reinterpret_cast<const bf16x8*>(q + 2 * PS);
+      f[2] = *reinterpret_cast<const bf16x8*>(q + 2 * pl3);
     } else {
-      f[0] = *reinterpret_cast<const bf16x8*>(&P[bq0 * PS + o]);
-      f[1] = *reinterpret_cast<const bf16x8*>(&P[bq1 * PS + o]);
-      f[2] = *reinterpret_cast<const bf16x8*>(&P[bq2 * PS + o]);
+      const int o = poff<MB>(posb[j] + toff, fhalf);
+      f[0] = *reinterpret_cast<const bf16x8*>(&P[o]);
+      f[1] = *reinterpret_cast<const bf16x8*>(&P[PS + o]);
+      f[2] = *reinterpret_cast<const bf16x8*>(&P[pl3 + o]);
     }
   };
 
@@ -264,7 +284,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
       for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 
   // the products of column block j (B fragments fb) with all of the wave's row blocks
-  auto mfma_j = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[3], int j) {
+  auto mfma_j = [&](const bf16x8 (&fa)[TM][NA], const bf16x8 (&fb)[3], int j) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if constexpr (MB == 32) {
@@ -276,17 +296,19 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i][j], 0, 0, 0);
       } else {
-        // (h|m)x(h|h) = hh + mh, (h|l)x(m|h) = hm + lh, (m|h)x(m|l) = mm + hl: lanes q < 2 carry
-        // the first 16-k half of the 32, q >= 2 the second (the same 16 channels)
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][t], fb[t], acc[i][j], 0, 0, 0);
+        // X2 x Y3 = (h|l)x(l|h) = hl + lh, X1 x Y2 = (h|m)x(m|m) = hm + mm, X1 x Y1 = (h|m)x(h|h) =
+        // hh + mh -- smallest first; lanes q < 2 carry the first 16-k half of the 32, q >= 2 the
+        // second (the same 16 channels)
+        const bf16x8 x2 = GANAMD_P16_ADUP ? fa[i][1] : fhi ? fa[i][1] : fa[i][0];
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, fb[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[0], acc[i][j], 0, 0, 0);
       }
     }
   };
 
   // prologue: the block's scales, chunk 0's patch and tap 0's A fragments
-  bf16x8 fa[2][TM][3];
+  bf16x8 fa[2][TM][NA];
   {
     f32x4 pv[UPT];
     patch_load(0, pv);
@@ -351,7 +373,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int q = 0; q < 3; ++q) fa[0][i][q] = fa[1][i][q];
+          for (int q = 0; q < NA; ++q) fa[0][i][q] = fa[1][i][q];
       }
     };
     // the tap loop: fully unrolled where the registers allow it (48-row blocks, the 4-wave W = 32
@@ -409,7 +431,8 @@ int occ_of() {
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
   if (a.W == 64) {
-    constexpr int NW = BM == 128 ? 8 : BM == 96 ? GANAMD_P96_NW : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
+    constexpr int NW = BM == 128 ? 8 : BM == 96 ? ((GANAMD_P96_MB == 16 && KK == 5) ? 8 : GANAMD_P96_NW)
+                                 : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
     if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
       hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),

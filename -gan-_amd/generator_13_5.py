@@ -370,16 +370,16 @@ class ResnetInit(nn.Module):
         with ops.Branches(x_res.device, 4 + (extra is not None)) as br:
             br.share(x_res, x_tr, None if extra is None else extra[1])
             with br[0]:
-                r_r = self.residual(x_res, w)
+                r_r = br.out(0, self.residual(x_res, w))
             with br[1]:
-                r_t = self.residual_across(x_res, w)
+                r_t = br.out(1, self.residual_across(x_res, w))
             with br[2]:
-                t_t = self.transient(x_tr, w)
+                t_t = br.out(2, self.transient(x_tr, w))
             with br[3]:
-                t_r = self.transient_across(x_tr, w)
+                t_r = br.out(3, self.transient_across(x_tr, w))
             if extra is not None:
                 with br[4]:
-                    e = extra[0](extra[1], w)
+                    e = br.out(4, extra[0](extra[1], w))
         out = (ops.add_prelu(r_r, t_r, self.activation_residual.weight),
                ops.add_prelu(r_t, t_t, self.activation_transient.weight))
         return out if extra is None else out + (e,)
