@@ -26,7 +26,7 @@ EPI_STORE, EPI_BIAS, EPI_DEMOD, EPI_ACCUM, EPI_SCALE = 0, 1, 2, 3, 4
 CONV_FWD, CONV_DGRAD, CONV_WGRAD = 0, 1, 2
 ACT_SIGMOID, ACT_TANH, ACT_LEAKY = 0, 1, 2
 MATH_F32, MATH_BF16 = 0, 1
-KERNEL_PATCH_FWD, KERNEL_PATCH_DGRAD, KERNEL_WGRAD_ROW = 1, 2, 4     # ganamd_conv_desc.kernel_off bits
+KERNEL_PATCH_FWD, KERNEL_PATCH_DGRAD, KERNEL_WGRAD_ROW, KERNEL_SMALL = 1, 2, 4, 8   # ganamd_conv_desc.kernel_off bits
 
 
 class ConvDesc(ctypes.Structure):

@@ -2229,7 +2229,8 @@ bool desc_ok(const ganamd_conv_desc* d) {
   return d && d->B > 0 && d->Cin > 0 && d->Cout > 0 && d->H > 0 && d->W > 0 && d->OH > 0 && d->OW > 0 &&
          d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0 &&
          (d->math == GANAMD_MATH_F32 || d->math == GANAMD_MATH_BF16) &&
-         (d->kernel_off & ~(GANAMD_KERNEL_PATCH_FWD | GANAMD_KERNEL_PATCH_DGRAD | GANAMD_KERNEL_WGRAD_ROW)) == 0 &&
+         (d->kernel_off & ~(GANAMD_KERNEL_PATCH_FWD | GANAMD_KERNEL_PATCH_DGRAD | GANAMD_KERNEL_WGRAD_ROW |
+                            GANAMD_KERNEL_SMALL)) == 0 &&
          extents_ok(d);
 }
 
@@ -2435,6 +2436,11 @@ static ganamd_pack_job pack_job(const ganamd_conv_desc* d, int op, const float* 
                          pack_x3(d, op) ? 1 : 0, 0};
 }
 
+// the direct conv of Cout <= 4 forwards (conv_small.hip): raw weights only (packed_w = 0)
+static bool small_fwd(const ganamd_conv_desc* d) {
+  return !(d->kernel_off & GANAMD_KERNEL_SMALL) && !d->packed_w && d->math == GANAMD_MATH_F32 && d->KH == d->KW &&
+         ganamd_small::domain(d->Cout, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->transposed);
+}
 // The row-blocked split6 weight gradient (conv_wgrad_row.hip) where its domain fits: fp32 math,
 // stride-1 same convs on 32 / 64-wide maps; the split-K partial sums reduced here.
 static bool wrow_ok(const ganamd_conv_desc* d) {
@@ -2516,6 +2522,13 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
     dgrad_gemm(d, &M, &N, &Ck, &T);
   const int mode = op == GANAMD_CONV_FWD ? fwd_mode(d) : dgrad_mode(d);
   const int Mp = op == GANAMD_CONV_FWD ? d->Cout : d->Cin;
+  if (op == GANAMD_CONV_FWD && small_fwd(d)) {
+    // kernel 2: the direct conv -- {M, pixels per block, blocks, 1, blocks, 1, input channels, blocks, -, CUs, 2}
+    const int th = 8, blocks = d->B * (d->H / th);
+    const int v[11] = {d->Cout, th * d->W, blocks, 1, blocks, 1, d->Cin, blocks, 1, num_cus(), 2};
+    for (int i = 0; i < 11; ++i) info[i] = v[i];
+    return GANAMD_OK;
+  }
   if (pack_x3(d, op) && patch_geometry(Mp, Ck, d->B, d->H, d->W, d->KH, d->stride, d->pad, d->OH, d->OW, d->math,
                                        d->kernel_off, op == GANAMD_CONV_DGRAD)) {
     ganamd_patch::Args a{};
@@ -2573,6 +2586,7 @@ int ganamd_conv_workspace(const ganamd_conv_desc* d, int op, size_t* bytes) {
   int M, N, Ck, T;
   *bytes = 0;
   if (op == GANAMD_CONV_FWD) {
+    if (small_fwd(d)) return GANAMD_OK;     // the direct conv needs no workspace
     fwd_gemm(d, &M, &N, &Ck, &T);
     *bytes = (d->packed_w ? 0 : align256(pack_bytes(M, Ck, d->KH * d->KW, pack_x3(d, op)))) +
              slab_bytes(M, N, Ck, T, fwd_mode(d), d->math == GANAMD_MATH_BF16);
@@ -2669,6 +2683,12 @@ int ganamd_conv_fwd_ex(const ganamd_conv_desc* d, const float* x, const float* w
                        size_t workspace_bytes, hipStream_t stream) {
   if (!desc_ok(d) || !x || !w || !y || (noise && !noise_scale)) return GANAMD_EINVAL;
   if (ws_check(d, GANAMD_CONV_FWD, workspace, workspace_bytes) != GANAMD_OK) return GANAMD_EINVAL;
+  if (small_fwd(d)) {
+    if (noise) return GANAMD_EINVAL;        // (no noisy conv has Cout <= 4)
+    const ganamd_small::Args a{x, x_scale, w, bias, y_scale, act_alpha, alpha, y, d->B, d->Cin, d->H, d->W,
+                               d->Cout, d->KH, d->pad, d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0};
+    return ganamd_small::launch(a, stream) == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
+  }
   ConvArgs p{};
   int M, N, Ck, T, sm, sc;
   fwd_gemm(d, &M, &N, &Ck, &T);
@@ -2864,11 +2884,11 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
                        d->H, d->W, d->pad);
     return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
+  float* ring = pad_bytes ? reinterpret_cast<float*>(ws) : nullptr;
+  const int Rn = Hp * Wp - d->H * d->W;
   p.g = Gather{gy, gy_scale, d->Cout, d->B, d->OH, d->OW, Hp, Wp, d->KW, d->stride, 0, kTransposed};
   p.y = gx;
   p.ohw = Hp * Wp;
-  float* ring = pad_bytes ? reinterpret_cast<float*>(ws) : nullptr;
-  const int Rn = Hp * Wp - d->H * d->W;
   if (d->pad > 0) {
     p.om = OutMap{-1, d->pad, d->H, Wp, Hp * Wp, d->W, d->H * d->W, Rn, (long)d->B * Rn, ring};
     p.ldy = (long)d->B * d->H * d->W;

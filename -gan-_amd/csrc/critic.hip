@@ -324,7 +324,8 @@ extern "C" {
 ganamd_critic_plan* ganamd_critic_create(const ganamd_critic_op* ops, int n_ops, int B, int C0, int H0, int W0,
                                          int segments, int math, int kernel_off) {
   if (!ops || n_ops <= 0 || B <= 0 || C0 <= 0 || H0 <= 0 || W0 <= 0 || segments <= 0 || B % segments) return nullptr;
-  if (kernel_off & ~(GANAMD_KERNEL_PATCH_FWD | GANAMD_KERNEL_PATCH_DGRAD | GANAMD_KERNEL_WGRAD_ROW)) return nullptr;
+  if (kernel_off & ~(GANAMD_KERNEL_PATCH_FWD | GANAMD_KERNEL_PATCH_DGRAD | GANAMD_KERNEL_WGRAD_ROW | GANAMD_KERNEL_SMALL))
+    return nullptr;
   auto* p = new ganamd_critic_plan();
   p->ops.assign(ops, ops + n_ops);
   p->B = B;

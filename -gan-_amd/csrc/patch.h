@@ -75,3 +75,26 @@ void plan(int M, int J, int B, int H, int W, int K, int segs, int cus, int* spli
 hipError_t launch(const Args& a, hipStream_t st);
 
 }  // namespace ganamd_wrow
+
+namespace ganamd_small {
+
+// One launch of the direct (vector-ALU, exact fp32) convolution for at most four output channels
+// (conv_small.hip): stride 1, "same" K x K (K = 1 / 3 / 5), CNHW x [C][B][H][W] -> y [M][B*H*W]
+//   y[m][b,oh,ow] = act(alpha * sum_{c,kh,kw} w[m][c][kh][kw] * xs(c, b, oh + kh - pad, ow + kw - pad)
+//                       * y_scale[m][b] + bias[m])      (xs = x * x_scale[c][b], padded)
+struct Args {
+  const float* x;
+  const float* x_scale;    // [C][B] or null
+  const float* w;          // [M][C][K][K], as stored (no packing)
+  const float* bias;       // [M] or null
+  const float* y_scale;    // [M][B] or null
+  const float* act;        // PReLU slopes [M] or null
+  float alpha;
+  float* y;
+  int B, C, H, W, M, K, pad, replicate;
+};
+
+bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW, int transposed);
+hipError_t launch(const Args& a, hipStream_t st);
+
+}  // namespace ganamd_small

@@ -95,20 +95,21 @@ def math_mode(mode: str):
 PLAN_FIELDS = ("bm", "bn", "gx", "gy", "nfull_t", "S", "kt_per_split", "blocks", "occupancy", "cus", "kernel")
 
 
-def set_patch(mask: int = 7) -> int:
-    """Which stride-1 convs this process's layers send to the split6 LDS-patch kernels (bit 0
-    forward, bit 1 dgrad, bit 2 the row-blocked weight gradient; default 7 = all; 0 = the gather
-    GEMMs, for A/B and tests).  It only sets the ``kernel_off`` field of the descriptors this module
-    builds (and of critic plans created afterwards): the library itself keeps no such state.  Like
-    ``math_mode`` it is read by the backward too (autograd runs it on its own threads), so it is
-    process-wide for the Python layers.  Returns the previous mask."""
-    prev = (~_KOFF[0]) & 7
-    _KOFF[0] = (~int(mask)) & 7
+def set_patch(mask: int = 15) -> int:
+    """Which convs this process's layers send to the specialised kernels (bit 0: stride-1 forwards
+    to the split6 LDS-patch conv, bit 1: their dgrads, bit 2: the row-blocked weight gradient, bit 3:
+    the direct conv of Cout <= 4 forwards; default 15 = all; 0 = the gather GEMMs, for A/B and
+    tests).  It only sets the ``kernel_off`` field of the descriptors this module builds (and of
+    critic plans created afterwards): the library itself keeps no such state.  Like ``math_mode`` it
+    is read by the backward too (autograd runs it on its own threads), so it is process-wide for the
+    Python layers.  Returns the previous mask."""
+    prev = (~_KOFF[0]) & 15
+    _KOFF[0] = (~int(mask)) & 15
     return prev
 
 
 @contextlib.contextmanager
-def patch_conv(mask: int = 7):
+def patch_conv(mask: int = 15):
     """``set_patch(mask)`` inside the block."""
     prev = set_patch(mask)
     try:
@@ -336,6 +337,14 @@ def _need(t, n, what):
         raise _lib.GanAmdError(f"{what}: expected {n} elements, got {tuple(t.shape)}")
 
 
+def small_fwd(geo: Geo) -> bool:
+    """Does ganamd_conv_fwd run this geometry as the direct conv of Cout <= 4 (csrc/conv_small.hip,
+    ToRGB)?  It takes the weights as stored, so the layers pass them unpacked."""
+    return (not geo.transposed and 1 <= geo.Cout <= 4 and geo.stride == 1 and geo.K in (1, 3, 5) and
+            geo.pad == (geo.K - 1) // 2 and geo.OH == geo.H and geo.OW == geo.W and geo.W == 64 and
+            geo.H % 8 == 0 and _MATH[0] == _lib.MATH_F32 and not (_KOFF[0] & _lib.KERNEL_SMALL))
+
+
 def _w_numel(geo):
     return geo.Cin * geo.Cout * geo.K * geo.K
 
@@ -351,7 +360,7 @@ def _conv_fwd(geo: Geo, x, w, bias=None, xs=None, ys=None, alpha=1.0, out=None):
         _need(out, geo.Cout * geo.B * geo.OH * geo.OW, "conv_fwd out")
     y = out if out is not None else torch.empty((geo.Cout, geo.B, geo.OH, geo.OW), device=x.device,
                                                 dtype=torch.float32)
-    pw = PackCache.get(geo, _lib.CONV_FWD, w)
+    pw = None if small_fwd(geo) else PackCache.get(geo, _lib.CONV_FWD, w)
     packed = pw is not None
     nb = geo.ws_bytes(_lib.CONV_FWD, packed)
     ws = workspace(nb, x.device) if nb else None

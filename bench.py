@@ -70,7 +70,8 @@ def parse():
                          "one graph per phase, the reference's order)")
     ap.add_argument("--patch", choices=["on", "off"], default="on",
                     help="stride-1 convs on 32/64-wide maps through the split6 LDS-patch conv and the row-blocked "
-                         "weight gradient (default) or the gather GEMMs (ops.set_patch 7 / 0: ganamd_conv_desc.kernel_off; A/B)")
+                         "weight gradient, Cout <= 4 forwards through the direct conv (default) or everything "
+                         "through the gather GEMMs (ops.set_patch 15 / 0: ganamd_conv_desc.kernel_off; A/B)")
     ap.add_argument("--fake-groups", default=None, metavar="K,K,...",
                     help="fake-batch groups of the n_critic steps, each one generator forward with segmented "
                          "BatchNorm (default: the headline schedule FAKE_GROUPS)")
@@ -437,7 +438,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     from gan_amd import ops
     from gan_amd.dist import allreduce_mean_
-    ops.set_patch(7 if args.patch == "on" else 0)     # patch fwd + dgrad, row-blocked wgrad (descriptor kernel_off)
+    ops.set_patch(15 if args.patch == "on" else 0)    # patch fwd + dgrad, row-blocked wgrad, direct Cout<=4 conv (kernel_off)
 
     G, D, tr, it = build(args, dev, rank, world)
     B = args.batch

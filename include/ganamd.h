@@ -67,6 +67,7 @@ typedef struct ganamd_conv_desc {
 #define GANAMD_KERNEL_PATCH_FWD 1
 #define GANAMD_KERNEL_PATCH_DGRAD 2
 #define GANAMD_KERNEL_WGRAD_ROW 4
+#define GANAMD_KERNEL_SMALL 8     /* the direct vector-ALU conv of Cout <= 4 forwards (ToRGB, csrc/conv_small.hip) */
 
 /* Workspace bytes needed by op (GANAMD_CONV_FWD/DGRAD/WGRAD).  Every entry point that takes a
  * workspace also takes its size in bytes and returns GANAMD_EINVAL (launching nothing) when it is

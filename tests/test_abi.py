@@ -60,8 +60,13 @@ def test_workspace_sizes():
     assert L.ganamd_rowreduce_workspace(8, 4096) >= 8 * 3 * 4
     bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 7, 0)   # unknown math mode
     assert L.ganamd_conv_workspace(bad, _lib.CONV_FWD, n) == -1
-    bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 0, 8)   # unknown kernel_off bit
+    bad = _lib.ConvDesc(4, 8, 16, 16, 8, 16, 16, 3, 3, 1, 1, 1, 0, 0, 0, 16)  # unknown kernel_off bit
     assert L.ganamd_conv_workspace(bad, _lib.CONV_FWD, n) == -1
+    # the direct conv of Cout <= 4 forwards (raw weights) needs none; packed weights take the GEMM
+    rgb = _lib.ConvDesc(4, 108, 64, 64, 3, 64, 64, 5, 5, 1, 2, 1, 0, 0, 0, 0)
+    assert L.ganamd_conv_workspace(rgb, _lib.CONV_FWD, n) == 0 and n.value == 0
+    rgb = _lib.ConvDesc(4, 108, 64, 64, 3, 64, 64, 5, 5, 1, 2, 1, 0, 0, 0, _lib.KERNEL_SMALL)
+    assert L.ganamd_conv_workspace(rgb, _lib.CONV_FWD, n) == 0 and n.value > 0
 
 
 @pytest.mark.parametrize("bad", ["x", "w"])

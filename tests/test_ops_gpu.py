@@ -1160,3 +1160,44 @@ def test_kernel_selection_per_call_threads(ops):
     for k in range(2):
         for y in outs[k]:
             assert torch.equal(y, single[k]), k
+
+
+SMALL_CASES = [
+    # B, Cin, H, Cout, k, pad mode, scaled: the direct conv of Cout <= 4 forwards (conv_small.hip)
+    (4, 108, 64, 3, 5, 1, False),    # ToRGB at 64x64 (pad mode 1: replicate)
+    (4, 108, 64, 3, 5, 1, True),     # modulated-style scales
+    (3, 20, 64, 4, 3, 0, False),     # zero padding, 3x3, four outputs, a channel tail
+    (2, 9, 64, 1, 1, 0, True),       # 1x1, one output, a channel tail
+]
+
+
+@pytest.mark.parametrize("case", SMALL_CASES)
+def test_small_cout_conv(ops, case):
+    """The direct vector-ALU conv (Cout <= 4: ToRGB, generator_13_5.py:470-493) against float64:
+    plan_info reports it (kernel 2), it needs no workspace, and its error is at most that of a
+    sequential fp32 FMA convolution (it IS one: channel, kernel row, kernel column order) or 1e-6."""
+    from gan_amd import _lib
+    from tests._emu import emulate, max_rel, seq_fp32
+    B, cin, H, cout, k, mode, scaled = case
+    g = ops.conv_geo(B, cin, H, H, cout, k, 1, (k - 1) // 2, mode)
+    info = ops.plan_info(g, 0, scaled)
+    assert info["kernel"] == 2 and g.ws_bytes(_lib.CONV_FWD) == 0, info
+    assert ops.plan_info(ops.conv_geo(B, cin, 32, 32, cout, k, 1, (k - 1) // 2, mode), 0, scaled)["kernel"] != 2
+    gen = torch.Generator().manual_seed(700 + SMALL_CASES.index(case))
+    x = torch.randn(cin, B, H, H, generator=gen).to(DEV)
+    w = torch.nn.Parameter(torch.randn(cout, cin, k, k, generator=gen).to(DEV))
+    bias = torch.randn(cout, generator=gen).to(DEV)
+    xs = (torch.rand(cin, B, generator=gen) + 0.5).to(DEV) if scaled else None
+    ys = (torch.rand(cout, B, generator=gen) + 0.5).to(DEV) if scaled else None
+    with torch.no_grad():
+        got = ops._conv_fwd(g, x, w, bias, xs, ys, 0.7)
+    torch.cuda.synchronize()
+    ref = emulate("fwd", g, x=x, w=w, xs=xs, ys=ys, alpha=0.7, bias=bias)
+    e = max_rel(got, ref)
+    eseq = max_rel(seq_fp32("fwd", g, x=x, w=w, xs=xs, ys=ys, alpha=0.7) + bias[:, None, None, None], ref)
+    print(f"{case}: max rel err vs float64 {e:.2e} (sequential fp32 FMA {eseq:.2e})")
+    assert e <= max(1e-6, 2 * eseq), (e, eseq)
+    with torch.no_grad(), ops.patch_conv(7):        # the same conv on the gather GEMM (bit 3 off)
+        other = ops._conv_fwd(g, x, w, bias, xs, ys, 0.7)
+    assert ops.plan_info(g, 0, scaled)["kernel"] == 2
+    assert max_rel(other, ref) < 1e-5

@@ -100,7 +100,7 @@ def main(B):
         print(f"== {tag}", flush=True)
         _g_twice(tr, snap, G, B)
     ops.BRANCH_STREAMS[0] = True
-    ops.set_patch(7)
+    ops.set_patch(15)
     if os.environ.get("DET_FULL") != "1":
         return
 

@@ -31,7 +31,7 @@ def run():
     args.batch = bench.CONFIGS[args.config][1]
     args.precision = "fp32"
     from gan_amd import ops
-    ops.set_patch(7)
+    ops.set_patch(15)
     dev = torch.device("cuda", 0)
     G, D, tr, it = bench.build(args, dev, 0, 1)
     it.eager()
