@@ -2541,7 +2541,7 @@ int ganamd_conv_plan_info(const ganamd_conv_desc* d, int op, int scaled, int* in
     a.scale = scaled ? reinterpret_cast<const float*>(info) : nullptr;   // selects the instance only
     const int bm = ganamd_patch::row_tile(Mp), gy = (Mp + bm - 1) / bm;
     const int blocks = (int)ganamd_patch::blocks(a), gx = blocks / gy;
-    const int v[11] = {bm, ganamd_patch::block_pixels(d->W), gx, gy, gx, 1, ((Ck + BK - 1) / BK) * T, blocks,
+    const int v[11] = {bm, ganamd_patch::block_pixels(d->W, d->B, d->H), gx, gy, gx, 1, ((Ck + BK - 1) / BK) * T, blocks,
                        ganamd_patch::occupancy(a), num_cus(), 1};
     for (int i = 0; i < 11; ++i) info[i] = v[i];
     return GANAMD_OK;

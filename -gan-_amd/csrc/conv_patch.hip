@@ -70,6 +70,9 @@ constexpr int kMaxScale = 1024;   // input channels whose scales the block stage
 #ifndef GANAMD_P128
 #define GANAMD_P128 0             // a 128-row tile for 96 < M <= 128 (else the gather GEMM takes the conv)
 #endif
+#ifndef GANAMD_P32_TALL
+#define GANAMD_P32_TALL 1         // W = 32 on large grids: 16-row (512-pixel) blocks, the W = 64 wave layouts
+#endif
 #ifndef GANAMD_P64_NW
 #define GANAMD_P64_NW 8           // waves of a 64-row block at W = 64 (8: 2 along M x 4 along pixels)
 #endif
@@ -123,7 +126,7 @@ __device__ __forceinline__ int mfma_row(int lane, int r) {
 template <int BM, int NW, int NPIX, int KK, int TW, bool BSCALE, bool DGRAD>
 __global__ __launch_bounds__(64 * NW) void conv_patch_x3_kernel(Args p) {
   constexpr int NT = 64 * NW;
-  constexpr int MB = (BM % 32 == 0) ? ((BM == 96 && TW == 64 && KK == 5) ? GANAMD_P96_MB : 32) : 16;   // MFMA block edge (48 rows: 16)
+  constexpr int MB = (BM % 32 == 0) ? ((BM == 96 && NPIX == 512 && KK == 5) ? GANAMD_P96_MB : 32) : 16;   // MFMA block edge (48 rows: 16)
   // waves along M: blocks of 4 waves per 32 rows (the 12-wave 96-row and 8-wave 64-row blocks) give
   // each wave 32 rows x 128 pixels (a third / half of the weight fragments per wave, 3 / 2 waves per
   // SIMD); the 8-wave 96-row block on 16x16 fragments gives each wave 48 rows x 128 pixels (2 waves
@@ -427,15 +430,25 @@ int occ_of() {
   return v;
 }
 
-// instance selection: W = 64 -> 512 pixels / 8 waves, W = 32 -> 256 pixels / 4 waves
+// instance selection: W = 64 -> 512 pixels (8 rows) / 8-12 waves; W = 32 on large grids -> 512 pixels
+// (16 rows) with the same waves; W = 32 otherwise -> 256 pixels / 4 waves
+template <int BM, int KK>
+constexpr int nw512() {
+  return BM == 128 ? 8 : BM == 96 ? ((GANAMD_P96_MB == 16 && KK == 5) ? 8 : GANAMD_P96_NW)
+                   : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
+}
 template <int BM, int KK, bool BSCALE, bool DGRAD>
 hipError_t go(const Args& a, hipStream_t st, bool dry, int* occ) {
+  constexpr int NW = nw512<BM, KK>();
   if (a.W == 64) {
-    constexpr int NW = BM == 128 ? 8 : BM == 96 ? ((GANAMD_P96_MB == 16 && KK == 5) ? 8 : GANAMD_P96_NW)
-                                 : BM == 64 ? GANAMD_P64_NW : GANAMD_P48_NW;
     if (occ) *occ = occ_of<BM, NW, 512, KK, 64, BSCALE, DGRAD>();
     if (!dry)
       hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 64, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),
+                         dim3(64 * NW), 0, st, a);
+  } else if (block_pixels(a.W, a.B, a.H) == 512) {
+    if (occ) *occ = occ_of<BM, NW, 512, KK, 32, BSCALE, DGRAD>();
+    if (!dry)
+      hipLaunchKernelGGL((conv_patch_x3_kernel<BM, NW, 512, KK, 32, BSCALE, DGRAD>), dim3((unsigned)blocks(a)),
                          dim3(64 * NW), 0, st, a);
   } else {
     constexpr int NW = BM == 128 ? 8 : 4;     // 128 rows: 2 waves along M x 4 along pixels
@@ -473,16 +486,20 @@ int row_tile(int M) {
   return M <= 0 ? 0 : M <= 48 ? 48 : (GANAMD_P64 && M <= 64) ? 64 : M <= 96 ? 96 : (GANAMD_P128 && M <= 128) ? 128 : 0;
 }
 
-int block_pixels(int W) { return W == 64 ? 512 : W == 32 ? 256 : 0; }
+// W = 32: 16-row blocks when the grid still has two rounds of them (B * H / 16 >= 512: the fake
+// batches' 256-sample forward), else 8-row blocks
+int block_pixels(int W, int B, int H) {
+  return W == 64 ? 512 : W == 32 ? ((GANAMD_P32_TALL && H % 16 == 0 && (long)B * H / 16 >= 512) ? 512 : 256) : 0;
+}
 
 bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW) {
   if (stride != 1 || (K != 3 && K != 5) || pad != (K - 1) / 2 || OH != H || OW != W || (W != 32 && W != 64))
     return false;
-  return row_tile(M) != 0 && H % (block_pixels(W) / W) == 0;
+  return row_tile(M) != 0 && H % (block_pixels(W, 1, H) / W) == 0;
 }
 
 long blocks(const Args& a) {
-  const int bm = row_tile(a.M), th = block_pixels(a.W) / a.W;
+  const int bm = row_tile(a.M), th = block_pixels(a.W, a.B, a.H) / a.W;
   return (long)((a.M + bm - 1) / bm) * a.B * (a.H / th);
 }
 

@@ -32,8 +32,9 @@ struct Args {
 
 // The row tile for M rows (48 or 96), 0 when the patch kernel does not take M.
 int row_tile(int M);
-// Pixels per block for map width W (the block covers whole rows of one image).
-int block_pixels(int W);
+// Pixels per block for map width W (the block covers whole rows of one image; W = 32: 16 rows on
+// grids of B * H / 16 >= 512 blocks, else 8).
+int block_pixels(int W, int B, int H);
 // The kernel's domain (the packing and the dispatch agree through it): stride 1, same padding,
 // K = 3 / 5, square, W = 32 / 64, H a multiple of the block's rows, M <= 96.
 bool domain(int M, int H, int W, int K, int stride, int pad, int OH, int OW);

@@ -53,6 +53,14 @@ SHAPES_PATCH = [   # the LDS-patch conv's instances (AB_SET=patch)
     ("dgrad", 64, 96, 64, 96, 5, 1, 2, False, 10),
     ("dgrad", 128, 64, 64, 64, 3, 1, 1, False, 25),
 ]
+SHAPES_P32 = [   # the patch conv at W = 32 on the fake batches' 256-sample grid (AB_SET=p32)
+    ("fwd", 256, 96, 32, 96, 5, 1, 2, True, 10),
+    ("fwd", 256, 96, 32, 96, 3, 1, 1, True, 10),
+    ("fwd", 256, 48, 32, 48, 5, 1, 2, True, 20),
+    ("fwd", 256, 48, 32, 48, 3, 1, 1, True, 30),
+    ("fwd", 256, 48, 32, 54, 3, 1, 1, True, 10),
+    ("fwd", 64, 96, 32, 96, 5, 1, 2, True, 20),
+]
 SHAPES = [  # (op, B, cin, H, cout, k, stride, pad, scaled, weight = launches per iteration)
     ("fwd", 64, 96, 64, 96, 5, 1, 2, True, 60),
     ("fwd", 64, 48, 64, 48, 5, 1, 2, True, 120),
@@ -80,7 +88,7 @@ def accuracy():
     dev = torch.device("cuda")
     gen = torch.Generator().manual_seed(0)
     worst = 0.0
-    for op, B, cin, H, cout, k, s, p, scaled, n in {"patch": SHAPES_PATCH}.get(_os.environ.get("AB_SET"), SHAPES):
+    for op, B, cin, H, cout, k, s, p, scaled, n in {"patch": SHAPES_PATCH, "p32": SHAPES_P32}.get(_os.environ.get("AB_SET"), SHAPES):
         B = 2
         g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
         x = torch.randn(B, cin, H, H, generator=gen, dtype=torch.float64, requires_grad=True)
@@ -119,7 +127,7 @@ def child():
     from gan_amd import ops
     dev = torch.device("cuda")
     tot_t = tot_f = 0.0
-    for op, B, cin, H, cout, k, s, p, scaled, n in {"wgrad": SHAPES_WGRAD, "dg": SHAPES_DG, "patch": SHAPES_PATCH, "wide": SHAPES_WIDE}.get(_os.environ.get("AB_SET"), SHAPES):
+    for op, B, cin, H, cout, k, s, p, scaled, n in {"wgrad": SHAPES_WGRAD, "dg": SHAPES_DG, "patch": SHAPES_PATCH, "wide": SHAPES_WIDE, "p32": SHAPES_P32}.get(_os.environ.get("AB_SET"), SHAPES):
         g = ops.conv_geo(B, cin, H, H, cout, k, s, p)
         x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
         y = torch.randn(g.Cout, g.B, g.OH, g.OW, device=dev)
