@@ -195,7 +195,9 @@ def cpu_baseline(threads, B=8):
 #             launch of the critic's gather GEMM conv_gemm_kernel<128,128,2,2,1,false,false> (the
 #             plan keeps the 128x128 tile at this batch: the 128x256 one would leave 1.5 rounds);
 #   dominant  G13_5's 96-channel 5x5 modulated conv at 64x64 (x*s on the patch, *d in the
-#             epilogue), B = 64: one launch of the split6 LDS-patch conv conv_patch_x3_kernel<96,...>
+#             epilogue): launches of the split6 LDS-patch conv conv_patch_x3_kernel<96,...> at each
+#             batch the iteration runs it at (round 6: B = 256 x 10 and B = 64 x 20 per iteration,
+#             DOMINANT_MIX), averaged with those launch counts as weights
 #             -- the top kernel FAMILY (the patch conv: 0.54 s of the iteration's 1.80 s busy), the
 #             top single shape and, since round 5, the top kernel INSTANCE of the iteration trace
 #             (profiles/r05_iteration_summary.txt: 0.107 s over 30 launches; round 4's top instance
@@ -220,9 +222,9 @@ def _whole_tile_geo(ops, spec):
     raise RuntimeError(f"no whole-tile batch for {spec['shape']}")
 
 
-def probe_kernel(dev, spec, reps=20):
+def probe_kernel(dev, spec, reps=20, batch=None):
     import gan_amd.ops as ops
-    g, pl = _whole_tile_geo(ops, spec)
+    g, pl = _whole_tile_geo(ops, dict(spec, B=batch) if batch else spec)
     x = torch.randn(g.Cin, g.B, g.H, g.W, device=dev)
     w = torch.nn.Parameter(torch.randn(g.Cout, g.Cin, g.K, g.K, device=dev))
     xs = torch.rand(g.Cin, g.B, device=dev) if spec["scaled"] else None
@@ -279,16 +281,58 @@ TOP_INSTANCE = {"kernel": "conv_patch_x3_kernel<96, 12, 512, 5, 64, true, false>
                 "family_s": 0.538, "source": "profiles/r05_iteration_summary.txt"}
 
 
-def roofline_probe(dev):
-    """The line's roofline object is the DOMINANT kernel's; the critic probe rides along."""
-    out = probe_kernel(dev, PROBES["dominant"])
-    # HBM bytes per launch from rocprofv3 PMC passes of this launch (tools/pmc_traffic.sh), if recorded
+# The batches the iteration launches the dominant kernel at, and how often (the census of one
+# iteration, profiles/r04_gemm_census.txt: 10 launches at B = 256 in the batched fake forward, 20 at
+# B = 64 in the single-batch fake forward and the generator step) -- used when no live census is given.
+DOMINANT_MIX = {256: 10, 64: 20}
+
+
+def dominant_mix(rec):
+    """{batch: launches per iteration} of the dominant shape, from the warm-up iteration's record."""
+    spec, mix = PROBES["dominant"], {}
+    for op, g, xs, ys, math in rec or ():
+        if (op == "fwd" and math == "fp32" and bool(xs) == spec["scaled"] and not g.transposed and g.Cin == spec["cin"]
+                and g.Cout == spec["cout"] and g.K == spec["k"] and g.H == spec["h"] and g.stride == 1):
+            mix[g.B] = mix.get(g.B, 0) + 1
+    return mix or dict(DOMINANT_MIX)
+
+
+def roofline_probe(dev, rec=None):
+    """The line's roofline object is the DOMINANT kernel's, over the batches the iteration launches
+    it at: each batch is probed on its own (20 launches, one event pair each) and the launches are
+    weighted by their count per iteration -- achieved = sum(n_B * FLOPs_B) / sum(n_B * us_B), i.e.
+    the average launch's algorithmic FLOPs over the average launch's duration, as a kernel trace of
+    the iteration would average them.  The critic probe rides along."""
+    mix = dominant_mix(rec)
+    per = [dict(probe_kernel(dev, PROBES["dominant"], batch=b), count=n) for b, n in sorted(mix.items(), reverse=True)]
+    assert len({p["kernel"] for p in per}) == 1, [p["kernel"] for p in per]
+    n = sum(p["count"] for p in per)
+    flop = sum(p["count"] * p["algorithmic_gflop_per_launch"] for p in per) / n
+    us = sum(p["count"] * p["launch_us"] for p in per) / n
+    out = dict(per[0])
+    out.update({"shape": PROBES["dominant"]["shape"].replace(f"B={PROBES['dominant']['B']}", "B=" + "/".join(
+                    str(p["batch"]) for p in per)) + " at its launch mix",
+                "batch": {str(p["batch"]): p["count"] for p in per}, "algorithmic_gflop_per_launch": flop,
+                "launch_us": us, "achieved": flop / us * 1e3, "frac": flop / us * 1e3 / SPLIT6_PIPE_PEAK_TFLOPS,
+                "frac_fp32": flop / us * 1e3 / FP32_MFMA_PEAK_TFLOPS,
+                "per_batch": [{k: p[k] for k in ("batch", "count", "blocks", "algorithmic_gflop_per_launch", "launch_us",
+                                                  "launch_us_min", "launch_us_back_to_back", "achieved", "frac")}
+                              for p in per],
+                "method": "each batch the iteration launches this kernel at (count per iteration from the warm-up "
+                          "iteration's census): 20 launches on the bench's stream, one HIP event pair each; achieved = "
+                          "launch-count-weighted FLOPs / launch-count-weighted mean duration"})
+    for k in ("blocks", "count", "launch_us_min", "launch_us_back_to_back"):
+        out.pop(k, None)
+    # HBM bytes per launch from rocprofv3 PMC passes of these launches (tools/pmc_traffic.sh), if
+    # recorded for every batch of the mix: the count-weighted mean per launch, like achieved
     tfile = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "roofline_traffic.json")
     if os.path.exists(tfile):
         t = json.load(open(tfile))
-        if t.get("kernel") == out["kernel"] and t.get("batch") == out["batch"]:
-            out["traffic"] = t.get("bytes_per_launch")
-            out["algorithmic_bytes_per_launch"] = t.get("algorithmic_bytes")
+        tb = t.get("per_batch", {})
+        if t.get("kernel") == out["kernel"] and all(str(p["batch"]) in tb for p in per):
+            out["traffic"] = sum(p["count"] * tb[str(p["batch"])]["bytes_per_launch"] for p in per) / n
+            out["algorithmic_bytes_per_launch"] = sum(p["count"] * tb[str(p["batch"])]["algorithmic_bytes"]
+                                                      for p in per) / n
             out["traffic_source"] = t.get("source")
     out["critic_probe"] = probe_kernel(dev, PROBES["probe"])
     out["top_instance"] = TOP_INSTANCE
@@ -578,7 +622,7 @@ def main():
     if "phase_frac" not in locals():
         phase_frac = None
     if rank == 0 and world == 1 and headline and not args.no_extras:
-        probe = roofline_probe(dev)
+        probe = roofline_probe(dev, census_rec)
     if rank == 0 and world == 1 and not args.no_extras:
         census = gemm_census(dev, census_rec)
     if rank == 0:
