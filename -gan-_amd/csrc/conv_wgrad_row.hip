@@ -53,6 +53,21 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, int off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// After each unit's LDS stores the wave waits for them to complete (lgkmcnt(0)) before the next
+// unit's split rewrites its registers.  Every variant of this kernel whose schedule moved (the
+// round-5 all-kernel-rows rewrite, a two-stage register prefetch, hoisted load offsets) made the
+// 96 -> 96 3x3 64x64 scaled instance sum differently run to run, always in A rows that lanes 48-63
+// of a unit store; with this wait the hoisted-offset variant passes 8 of 8 determinism runs
+// (without it 0 of 5, with 8-byte instead of 16-byte stores 4 of 5): profiles/r06_wrow_lds_store.txt.
+// The mechanism is not pinned down (the gather GEMM rewrites its store registers sooner and is
+// deterministic); the wait costs ~1.5 % of this kernel's time (126.4 -> 128.1 ms on the A/B set).
+#ifndef GANAMD_WROW_DRAIN
+#define GANAMD_WROW_DRAIN 1
+#endif
+__device__ __forceinline__ void lds_store_drain() {
+  if (GANAMD_WROW_DRAIN) __builtin_amdgcn_s_waitcnt(0xC07F);   // vmcnt 63, expcnt 7, lgkmcnt 0
+}
+
 // exact 3-way split x = h + m + l (RNE; both differences exact in fp32)
 template <int N, class V>
 __device__ __forceinline__ void split3(const float* x, V& h, V& m, V& l) {
@@ -208,6 +223,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
         *reinterpret_cast<bf16x8*>(d) = h;
         *reinterpret_cast<bf16x8*>(d + PSA) = m;
         *reinterpret_cast<bf16x8*>(d + 2 * PSA) = l;
+        lds_store_drain();
       }
     }
 #pragma unroll
@@ -225,6 +241,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_row_kernel(Args p) {
         *reinterpret_cast<bf16x4*>(d) = h;
         *reinterpret_cast<bf16x4*>(d + PSB) = m;
         *reinterpret_cast<bf16x4*>(d + 2 * PSB) = l;
+        lds_store_drain();
       }
     }
   };

@@ -27,6 +27,8 @@ SHAPES_WGRAD = [
     ("wgrad", 64, 64, 64, 64, 3, 1, 1, False, 50),
     ("wgrad", 128, 128, 32, 128, 3, 1, 1, False, 25),
     ("wgrad", 64, 128, 32, 128, 3, 1, 1, False, 50),
+    ("wgrad", 64, 96, 64, 96, 3, 1, 1, True, 10),
+    ("wgrad", 64, 96, 64, 48, 3, 1, 1, True, 20),
 ]
 SHAPES_DG = [   # fwd vs dgrad vs wgrad of the same critic convs (AB_SET=dg)
     ("fwd", 128, 64, 64, 64, 3, 1, 1, False, 25),

@@ -3,7 +3,8 @@
 set -e
 export TMPDIR=/tmp
 rm -rf /tmp/prof_sq
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES -d /tmp/prof_sq -o run --output-format csv -- python3 tools/gemm_micro.py "$@" > gpurun_out/sq_probe_run.log 2>&1
+CTRS=${SQ_COUNTERS:-"SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES"}
+timeout -s KILL 90 rocprofv3 --pmc $CTRS -d /tmp/prof_sq -o run --output-format csv -- python3 tools/gemm_micro.py "$@" > gpurun_out/sq_probe_run.log 2>&1
 C=$(find /tmp/prof_sq -name "*counter_collection.csv")
 python3 - "$C" <<'PY'
 import csv, sys, collections
