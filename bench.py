@@ -198,10 +198,10 @@ def cpu_baseline(threads, B=8):
 #             epilogue): launches of the split6 LDS-patch conv conv_patch_x3_kernel<96,...> at each
 #             batch the iteration runs it at (round 6: B = 256 x 10 and B = 64 x 20 per iteration,
 #             DOMINANT_MIX), averaged with those launch counts as weights
-#             -- the top kernel FAMILY (the patch conv: 0.54 s of the iteration's 1.80 s busy), the
+#             -- the top kernel FAMILY (the patch conv: 0.49 s of the iteration's 1.78 s busy), the
 #             top single shape and, since round 5, the top kernel INSTANCE of the iteration trace
-#             (profiles/r05_iteration_summary.txt: 0.107 s over 30 launches; round 4's top instance
-#             was the critic GEMM, now split between its 128x128 and 128x256 forms).  `top_instance`
+#             (profiles/r06_iteration_summary.txt: 0.112 s over 30 launches, the 8-wave paired
+#             16x16x32 form since round 6; round 4's top instance was the critic GEMM).  `top_instance`
 #             records which kernel leads the committed trace by instance.
 PROBES = {
     "probe": dict(B=96, cin=128, h=32, cout=128, k=3, scaled=False,
@@ -276,25 +276,9 @@ def probe_kernel(dev, spec, reps=20, batch=None):
 
 # Which probed kernel leads the committed iteration trace by instance (kernel name with template
 # arguments; tools/trace_summary.py), and by family -- from the profile of this round's build.
-TOP_INSTANCE = {"kernel": "conv_patch_x3_kernel<96, 12, 512, 5, 64, true, false>", "probe": "dominant",
-                "iteration_s": 0.107, "launches": 30, "family_top": "ganamd_patch::conv_patch_x3_kernel",
-                "family_s": 0.538, "source": "profiles/r05_iteration_summary.txt"}
-
-
-# The batches the iteration launches the dominant kernel at, and how often (the census of one
-# iteration, profiles/r04_gemm_census.txt: 10 launches at B = 256 in the batched fake forward, 20 at
-# B = 64 in the single-batch fake forward and the generator step) -- used when no live census is given.
-DOMINANT_MIX = {256: 10, 64: 20}
-
-
-def dominant_mix(rec):
-    """{batch: launches per iteration} of the dominant shape, from the warm-up iteration's record."""
-    spec, mix = PROBES["dominant"], {}
-    for op, g, xs, ys, math in rec or ():
-        if (op == "fwd" and math == "fp32" and bool(xs) == spec["scaled"] and not g.transposed and g.Cin == spec["cin"]
-                and g.Cout == spec["cout"] and g.K == spec["k"] and g.H == spec["h"] and g.stride == 1):
-            mix[g.B] = mix.get(g.B, 0) + 1
-    return mix or dict(DOMINANT_MIX)
+TOP_INSTANCE = {"kernel": "conv_patch_x3_kernel<96, 8, 512, 5, 64, true, false>", "probe": "dominant",
+                "iteration_s": 0.112, "launches": 30, "family_top": "ganamd_patch::conv_patch_x3_kernel",
+                "family_s": 0.488, "source": "profiles/r06_iteration_summary.txt"}
 
 
 def roofline_probe(dev, rec=None):
