@@ -14,7 +14,8 @@ and G does not change during the n_critic critic steps, so they need not be made
   (B = 64: k <= 4).
 * ``overlap=True``: group j + 1 is replayed on a second HIP stream while the
   critic steps of group j (critic passes, gradient penalty, N > 1: the RCCL all-reduce, AdamW) run
-  on the main stream.  Every group has its own graph, memory pool and output buffers.
+  on the main stream.  Every group has its own graph and output buffers; the groups share one
+  memory pool, apart from the critic and generator graphs' pool.
 
 Each critic step copies its fake batch into the critic graph's fixed input (3 MB).  ``overlap=False``
 with groups of 1 is the reference's order: one graph per phase, the fake batch made inside the
@@ -136,8 +137,12 @@ class Iteration:
                     bufs[j]["x"] = self._fakes(self.groups[j])
                 return f
 
-            g["fake"] = [self._capture(fakes(j), torch.cuda.graph_pool_handle() if self.overlap else pool)
-                         for j in range(len(self.groups))]
+            # with overlap the fake groups replay beside the critic graphs, so not in their pool; but
+            # never beside each other (group j + 1 is issued after group j on the stream that ran it,
+            # or on the side stream after it waited for the main one), in capture order: one pool for
+            # all of them (one per group held ~13 GB more at B = 64)
+            fpool = torch.cuda.graph_pool_handle() if self.overlap else pool
+            g["fake"] = [self._capture(fakes(j), fpool) for j in range(len(self.groups))]
             g["fake"][0].replay()                # a valid fake batch for the critic capture
             self.xin = bufs[0]["x"][0].clone()
             self.bufs = bufs

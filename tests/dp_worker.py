@@ -135,8 +135,18 @@ def main_graph(out):
     # captures of the others' would add up)
     for r in range(world):
         if r == rank:
+            if os.environ.get("DP_MEMLOG") == "1":
+                print(f"[rank {rank}] before capture: device free {torch.cuda.mem_get_info()[0] / 2**30:.1f} GiB, "
+                      f"reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB", flush=True)
             it.capture()
-            print(f"[rank {rank}] captured", flush=True)
+            # hand the eager warm-up's cached blocks back before the next rank captures (the graph
+            # pools stay): rank 0 at 139 GiB reserved left the second rank's capture 3 GiB short
+            torch.cuda.synchronize()
+            if os.environ.get("DP_NO_EMPTY") != "1":
+                torch.cuda.empty_cache()
+            free, _ = torch.cuda.mem_get_info()
+            print(f"[rank {rank}] captured: reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB, device free "
+                  f"{free / 2**30:.1f} GiB", flush=True)
         dist.barrier()
     _mem("captured")
     restore(tr, snap)

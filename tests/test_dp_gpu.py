@@ -41,6 +41,19 @@ import torch
 from tests import dp_worker
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _release_gpu_cache():
+    """The ranks share this process's GPU: hand back what earlier tests in this process left cached
+    (the in-process reference runs of B = 64 models hold tens of GB), before and after each test --
+    eight ranks that started after the 2-rank B = 64 test's reference ran out of memory otherwise."""
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+    yield
+    gc.collect()
+    torch.cuda.empty_cache()
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -127,6 +140,9 @@ def test_dp_graph_iteration_matches_shard_mean(tmp_path, schedule, B):
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dp_worker.py"), out,
            "graph", schedule, str(B)]
     r = subprocess.run(cmd, cwd=REPO, env=_env(), timeout=900, capture_output=True, text=True)
+    if r.returncode != 0 and os.path.isdir(os.path.join(REPO, "gpurun_out")):   # the whole log, for the record
+        with open(os.path.join(REPO, "gpurun_out", f"dp_graph_{schedule}_{B}_fail.log"), "w") as f:
+            f.write(r.stdout + "\n==== stderr\n" + r.stderr)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = torch.load(out, weights_only=True)
     assert got["world"] == 2 and got["batch"] == B and got["d_grad0"] is not None
