@@ -1385,9 +1385,14 @@ __global__ void ring_fold_kernel(const float* __restrict__ ring, float* __restri
 // stride-2 tap of the wrong parity), a run of outputs at a replication-padded edge.  Input row i
 // is read by output row oh through tap kh iff clamp(oh*s - pad + kh) lies in [lo, hi], where
 // lo = hi = i, except that a replicated edge row also takes every position beyond the edge.
-template <typename I>
+//
+// SK, KK != 0: stride and (square) kernel size as compile-time constants -- the tap bounds' divisions
+// by the stride become shifts and the tap loops unroll (the generic form spends most of its time in
+// four runtime integer divisions per tap, not in its loads).  Same loop and summation order.
+template <typename I, int SK = 0, int KK = 0>
 __global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict__ gx, int C, int B, int H, int W,
-                                  int OH, int OW, int KH, int KW, int stride, int pad, int replicate) {
+                                  int OH, int OW, int KH_, int KW_, int stride_, int pad, int replicate) {
+  const int stride = SK ? SK : stride_, KH = KK ? KK : KH_, KW = KK ? KK : KW_;
   const I total = (I)C * B * H * W;
   const int T = KH * KW;
   constexpr int kFar = 1 << 20;
@@ -1402,11 +1407,13 @@ __global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict
     const int ilo = (replicate && i == 0) ? -kFar : i, ihi = (replicate && i == H - 1) ? kFar : i;
     const int jlo = (replicate && j == 0) ? -kFar : j, jhi = (replicate && j == W - 1) ? kFar : j;
     float acc = 0.f;
+#pragma unroll
     for (int kh = 0; kh < KH; ++kh) {
       // oh*s in [ilo + pad - kh, ihi + pad - kh]
       const int a0 = ilo + pad - kh, a1 = ihi + pad - kh;
       const int h0 = max(0, a0 <= 0 ? 0 : (a0 + stride - 1) / stride);
       const int h1 = min(OH - 1, a1 < 0 ? -1 : a1 / stride);
+#pragma unroll
       for (int kw = 0; kw < KW; ++kw) {
         const int b0 = jlo + pad - kw, b1 = jhi + pad - kw;
         const int w0 = max(0, b0 <= 0 ? 0 : (b0 + stride - 1) / stride);
@@ -1475,7 +1482,10 @@ double list_makespan(long F, double L, long R, double d, long slots);
 
 // Price of the extra reduce launch of a split GEMM (its own ~5 us run time on tiny data plus the
 // dependent-launch boundary).
-constexpr double reduce_launch_us() { return 3.0; }
+#ifndef GANAMD_REDUCE_US
+#define GANAMD_REDUCE_US 3.0
+#endif
+constexpr double reduce_launch_us() { return GANAMD_REDUCE_US; }
 
 // wgrad split-K by a small cost model: a GEMM of `tiles` output tiles, each `kt_total` K-steps of
 // `kflop` FLOPs, runs in ceil(tiles*s / slots) rounds of blocks (slots = resident blocks per CU
@@ -1608,7 +1618,10 @@ double list_makespan(long F, double L, long R, double d, long slots) {
   }
 }
 
-constexpr double kSustainedTflops = 150.0;   // chip-wide fp32 rate of the GEMM body (split6), all slots busy
+#ifndef GANAMD_SUSTAINED_TFLOPS
+#define GANAMD_SUSTAINED_TFLOPS 150.0
+#endif
+constexpr double kSustainedTflops = GANAMD_SUSTAINED_TFLOPS;   // chip-wide fp32 rate of the GEMM body (split6), all slots busy
 constexpr double kSustainedTflopsBf16 = 300.0;   // the bf16-LDS body (conv_body_bf16), gather-bound
 
 // The plan of one tile shape (bm x bn) and its modelled makespan in microseconds.
@@ -2832,10 +2845,14 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
     const long total = (long)d->Cin * d->B * d->H * d->W;
     const int rep = d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0;
-    if (total < (1L << 31) - (1L << 24))
-      hipLaunchKernelGGL(dgrad_fold_kernel<unsigned>, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B,
-                         d->H, d->W, d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, rep);
-    else
+    const bool k3 = d->KH == 3 && d->KW == 3;
+    if (total < (1L << 31) - (1L << 24)) {
+      auto fold = k3 && d->stride == 1 ? dgrad_fold_kernel<unsigned, 1, 3>
+                  : k3 && d->stride == 2 ? dgrad_fold_kernel<unsigned, 2, 3>
+                                         : dgrad_fold_kernel<unsigned>;
+      hipLaunchKernelGGL(fold, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H, d->W, d->OH, d->OW,
+                         d->KH, d->KW, d->stride, d->pad, rep);
+    } else
       hipLaunchKernelGGL(dgrad_fold_kernel<long>, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H,
                          d->W, d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, rep);
     return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
