@@ -1389,19 +1389,42 @@ __global__ void ring_fold_kernel(const float* __restrict__ ring, float* __restri
 // SK, KK != 0: stride and (square) kernel size as compile-time constants -- the tap bounds' divisions
 // by the stride become shifts and the tap loops unroll (the generic form spends most of its time in
 // four runtime integer divisions per tap, not in its loads).  Same loop and summation order.
+// The 32-bit instance (every index < 2^31) splits the element index with multiply-high divisions.
+struct Div31 {   // x / d for 0 <= x < 2^31: m = ceil(2^(31+l) / d), l = ceil(log2 d) (m < 2^32), q = mulhi(x, m) >> (l-1)
+  unsigned m = 0;
+  int s = 0;     // m == 0: d == 1
+  static Div31 of(unsigned d) {
+    Div31 r;
+    if (d <= 1) return r;
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    r.m = (unsigned)(((1ull << (31 + l)) + d - 1) / d);
+    r.s = l - 1;
+    return r;
+  }
+  __device__ __forceinline__ unsigned operator()(unsigned x) const { return m ? __umulhi(x, m) >> s : x; }
+};
+struct FoldDivs {
+  Div31 w, h, b;
+};
+
 template <typename I, int SK = 0, int KK = 0>
 __global__ void dgrad_fold_kernel(const float* __restrict__ Z, float* __restrict__ gx, int C, int B, int H, int W,
-                                  int OH, int OW, int KH_, int KW_, int stride_, int pad, int replicate) {
+                                  int OH, int OW, int KH_, int KW_, int stride_, int pad, int replicate, FoldDivs dv) {
   const int stride = SK ? SK : stride_, KH = KK ? KK : KH_, KW = KK ? KK : KW_;
   const I total = (I)C * B * H * W;
   const int T = KH * KW;
   constexpr int kFar = 1 << 20;
+  auto div = [](I x, I d, const Div31& f) -> I {
+    if constexpr (sizeof(I) == 4) return f(x);
+    return x / d;
+  };
   for (I idx = blockIdx.x * (I)blockDim.x + threadIdx.x; idx < total; idx += (I)gridDim.x * blockDim.x) {
-    const I r1 = idx / (I)W;
+    const I r1 = div(idx, (I)W, dv.w);
     const int j = (int)(idx - r1 * (I)W);
-    const I r2 = r1 / (I)H;
+    const I r2 = div(r1, (I)H, dv.h);
     const int i = (int)(r1 - r2 * (I)H);
-    const I c_ = r2 / (I)B;
+    const I c_ = div(r2, (I)B, dv.b);
     const int b = (int)(r2 - c_ * (I)B);
     const int c = (int)c_;
     const int ilo = (replicate && i == 0) ? -kFar : i, ihi = (replicate && i == H - 1) ? kFar : i;
@@ -2845,16 +2868,18 @@ int ganamd_conv_dgrad(const ganamd_conv_desc* d, const float* gy, const float* w
     if (dispatch_conv(p, pre, packed, slab, stream) != hipSuccess) return GANAMD_ELAUNCH;
     const long total = (long)d->Cin * d->B * d->H * d->W;
     const int rep = d->pad_mode == GANAMD_PAD_REPLICATE ? 1 : 0;
-    const bool k3 = d->KH == 3 && d->KW == 3;
+    const bool k3 = d->KH == 3 && d->KW == 3, k5 = d->KH == 5 && d->KW == 5;
+    const FoldDivs dv{Div31::of(d->W), Div31::of(d->H), Div31::of(d->B)};
     if (total < (1L << 31) - (1L << 24)) {
-      auto fold = k3 && d->stride == 1 ? dgrad_fold_kernel<unsigned, 1, 3>
+      auto fold = k3 && d->stride == 1   ? dgrad_fold_kernel<unsigned, 1, 3>
                   : k3 && d->stride == 2 ? dgrad_fold_kernel<unsigned, 2, 3>
+                  : k5 && d->stride == 1 ? dgrad_fold_kernel<unsigned, 1, 5>
                                          : dgrad_fold_kernel<unsigned>;
       hipLaunchKernelGGL(fold, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H, d->W, d->OH, d->OW,
-                         d->KH, d->KW, d->stride, d->pad, rep);
+                         d->KH, d->KW, d->stride, d->pad, rep, dv);
     } else
       hipLaunchKernelGGL(dgrad_fold_kernel<long>, dim3(grid1d(total)), dim3(256), 0, stream, Z, gx, d->Cin, d->B, d->H,
-                         d->W, d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, rep);
+                         d->W, d->OH, d->OW, d->KH, d->KW, d->stride, d->pad, rep, dv);
     return hipGetLastError() == hipSuccess ? GANAMD_OK : GANAMD_ELAUNCH;
   }
   if (d->transposed) {
