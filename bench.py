@@ -281,6 +281,22 @@ TOP_INSTANCE = {"kernel": "conv_patch_x3_kernel<96, 8, 512, 5, 64, true, false>"
                 "family_s": 0.488, "source": "profiles/r06_iteration_summary.txt"}
 
 
+# The batches the iteration launches the dominant kernel at, and how often (the census of one
+# iteration, profiles/r04_gemm_census.txt: 10 launches at B = 256 in the batched fake forward, 20 at
+# B = 64 in the single-batch fake forward and the generator step) -- used when no live census is given.
+DOMINANT_MIX = {256: 10, 64: 20}
+
+
+def dominant_mix(rec):
+    """{batch: launches per iteration} of the dominant shape, from the warm-up iteration's record."""
+    spec, mix = PROBES["dominant"], {}
+    for op, g, xs, ys, math in rec or ():
+        if (op == "fwd" and math == "fp32" and bool(xs) == spec["scaled"] and not g.transposed and g.Cin == spec["cin"]
+                and g.Cout == spec["cout"] and g.K == spec["k"] and g.H == spec["h"] and g.stride == 1):
+            mix[g.B] = mix.get(g.B, 0) + 1
+    return mix or dict(DOMINANT_MIX)
+
+
 def roofline_probe(dev, rec=None):
     """The line's roofline object is the DOMINANT kernel's, over the batches the iteration launches
     it at: each batch is probed on its own (20 launches, one event pair each) and the launches are
